@@ -1,0 +1,210 @@
+"""Benchmark: face-crops/s at 224x224, CViT forward on MI355X (BASELINE.json metric).
+
+One step = one CViT forward over a batch of 256 synthetic uint8 face crops
+already resident in HBM (config 2: B=256, pos slot j mod 32), through the C
+ABI, replayed from a hipGraph.  With N>1 ranks (torchrun, one process per GPU,
+backend nccl = RCCL) each rank scores its own 256-crop shard of the frame
+stream and the step ends with the config-3 exchange: an all-gather of the
+per-crop logits and the video score on every rank.  Whole-job crops/s =
+N*256*K / max-over-ranks time of K steps.
+
+Also printed on the same JSON line:
+  roofline      - the dominant conv kernel's achieved MFMA TFLOP/s (algorithmic
+                  FLOPs per launch / its average event-timed duration) vs the
+                  bf16/fp16 dense peak;
+  cpu_baseline  - the oracle's PyTorch CPU restatement of the reference forward
+                  (same CPU kernels as CViT-main/model/cvit.py), fp32, timed on
+                  a bounded sample on rank 0 at N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+from fac_fake_amd import _lib  # noqa: E402
+from fac_fake_amd.weights import STEM_CHANNELS, POOL_AFTER, make_crops, make_state_dict  # noqa: E402
+
+FLOP_PER_CROP = 13.2915e9          # 2 x (6.51726 G conv + 0.128455 G linear + 49,152 attn) MAC
+PEAK_TFLOPS = {"bf16": 2516.6, "fp16": 2516.6}  # 256 CU x 2.4 GHz x 4096 FLOP/clk/CU (dense, MI355X_MICROARCH)
+STAGE_NAMES = [f"conv{i + 1}" for i in range(17)] + ["patch_embed", "transformer", "head"]
+
+
+def conv_layer_flops(i: int, B: int) -> float:
+    """Algorithmic FLOPs of conv i (0-based) for B crops: 2*B*H*W*Cout*9*Cin."""
+    H = 224
+    for j in range(i):
+        if j in POOL_AFTER:
+            H //= 2
+    ci, co = STEM_CHANNELS[i]
+    return 2.0 * B * H * H * co * 9 * ci
+
+
+def cpu_baseline(sd, threads: int, iters: int = 4, batch: int = 32):
+    from oracle.cvit_torch import forward_fp32, normalize_u8
+    torch.set_num_threads(threads)
+    x = normalize_u8(make_crops(batch, seed=2))
+    forward_fp32(sd, x)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        forward_fp32(sd, x)
+    dt = time.perf_counter() - t0
+    return {"value": round(iters * batch / dt, 3), "unit": "face-crops/s", "cores": threads, "kind": "port",
+            "sample": f"{iters} x {batch} crops (fp32 PyTorch CPU restatement of cvit.py forward, "
+                      f"1 warm-up), torch {torch.__version__}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--stem-chunk", type=int, default=0)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    B = args.batch
+
+    lib = _lib.load()
+    sd = make_state_dict(0)
+    from fac_fake_amd.cvit import CViT
+    model = CViT(dtype=args.dtype)
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    model.to(dev)
+    model.reserve(B, dev)
+    if args.stem_chunk:
+        model.set_stem_chunk(args.stem_chunk)
+    ctx = model._ctx
+
+    crops = torch.from_numpy(make_crops(B, seed=3 + rank)).to(dev)      # synthetic, resident in HBM
+    pidx = (torch.arange(B, device=dev) % 32).to(torch.int32)
+    logits = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    score = torch.empty((), dtype=torch.float32, device=dev)
+    gathered = torch.empty(world * B, 2, dtype=torch.float32, device=dev)
+    stream = torch.cuda.Stream(dev)
+
+    def forward_on(s):
+        _lib.check(lib.fac_forward_nhwc_u8(ctx, crops.data_ptr(), B, pidx.data_ptr(), logits.data_ptr(), None,
+                                           s.cuda_stream), ctx, "forward")
+
+    graph = None
+    if not args.no_graph:
+        try:
+            stream.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(stream):
+                forward_on(stream)  # warm the code objects before capture
+            torch.cuda.synchronize(dev)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(stream):
+                with torch.cuda.graph(graph, stream=stream):
+                    forward_on(stream)
+        except Exception as e:  # eager launches are still the same kernels
+            print(f"[bench] graph capture failed, running eager: {e}", file=sys.stderr)
+            graph = None
+
+    def step():
+        with torch.cuda.stream(stream):
+            if graph is not None:
+                graph.replay()
+            else:
+                forward_on(stream)
+            if world > 1:
+                dist.all_gather_into_tensor(gathered, logits)
+                _lib.check(lib.fac_video_score(gathered.data_ptr(), world * B, score.data_ptr(), stream.cuda_stream),
+                           None, "video_score")
+            else:
+                _lib.check(lib.fac_video_score(logits.data_ptr(), B, score.data_ptr(), stream.cuda_stream),
+                           None, "video_score")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-stage event timing of one eager forward (same kernels, same stream)
+    stage_ms = (ctypes.c_float * 20)()
+    reps = 3
+    acc = np.zeros(20)
+    for _ in range(reps):
+        _lib.check(lib.fac_profile_forward_u8(ctx, crops.data_ptr(), B, pidx.data_ptr(), logits.data_ptr(), stage_ms,
+                                              20, stream.cuda_stream), ctx, "profile")
+        acc += np.frombuffer(stage_ms, dtype=np.float32)
+    acc /= reps
+    conv_ms = acc[:17]
+    dom = int(np.argmax(conv_ms))
+    dom_flops = conv_layer_flops(dom, B)
+    achieved = dom_flops / (conv_ms[dom] * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.dtype]
+
+    value = world * B * args.steps / elapsed
+    line = {
+        "metric": "face-crops/sec at 224x224 bf16, CViT forward, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "face-crops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic uint8 224x224 crops (splitmix64), deterministic synthetic CViT weights (no trained "
+                "checkpoint in the reference)",
+        "config": {"workload": "config 2: CViT forward, B=256 crops per GPU per step, pos slot j mod 32",
+                   "model": "CViT(224,7,2,512,1024,6,8,2048)", "global_batch": world * B, "seq_len": 2,
+                   "parallelism": f"frame-sharded x{world}" + (" + RCCL logit all-gather" if world > 1 else ""),
+                   "graph": graph is not None, "stem_chunk": args.stem_chunk},
+        "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
+        "roofline": {"bound": "mfma", "kernel": f"conv3x3_bn_relu ({STAGE_NAMES[dom]})",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "launch_ms": round(float(conv_ms[dom]), 4), "flops_per_launch": dom_flops},
+        "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, acc)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(sd, threads)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

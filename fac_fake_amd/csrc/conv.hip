@@ -1,0 +1,366 @@
+// Conv stem kernels: CViT.features (CViT-main/model/cvit.py:86-148), i.e.
+// 17 x [Conv2d 3x3 s1 p1 -> BatchNorm2d(eval) -> ReLU] with MaxPool2d(2,2)
+// after convs 3/6/9/13/17, computed as implicit GEMMs on MFMA.
+//
+// Layout: activations NHWC 16-bit (bf16 or fp16), BN folded into the conv
+// weights/bias at load time, fp32 accumulation, fp32 epilogue.
+//
+// GEMM view per conv: rows = output pixels of a TH x TW spatial box of one
+// image, cols = BN output channels, k = (tap, input channel).  A workgroup
+// stages the (TH+2) x (TW+2) input halo of a 32-channel chunk in LDS once and
+// reads all 9 taps from it (9x less L2 traffic than an im2col gather), while
+// per-tap weight slices [BN][32] stream through a second double buffer.
+//
+// Pixel order inside a box is "window-major" (4 consecutive GEMM rows = one
+// 2x2 pooling window), so in the 16x16x32 MFMA C layout (row = 4*(lane>>4) +
+// reg) each lane holds a whole window of one channel: the 2x2 max-pool is
+// three fmaxf in registers.
+#include "common.hpp"
+
+namespace fac {
+
+constexpr int CONV_CK = 32;           // input channels per K chunk
+constexpr int CONV_PS = CONV_CK + 8;  // LDS row stride (elements) = 80 B
+
+template <int TW>
+__device__ __forceinline__ void box_pixel(int m, int& py, int& px) {
+  constexpr int WW = TW / 2;
+  const int w = m >> 2, sub = m & 3;
+  const int wy = w / WW, wx = w - wy * WW;
+  py = 2 * wy + (sub >> 1);
+  px = 2 * wx + (sub & 1);
+}
+
+// Stage an OPIX x BN tile (row stride OPS, window-major rows) from LDS to
+// NHWC global memory with 16-byte stores in raster order.
+template <int TH, int TW, int BN, bool POOL>
+__device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, int b, int Ho, int Wo,
+                                           int oy0, int ox0, int Cout, int n0, int tid) {
+  constexpr int OTW = POOL ? TW / 2 : TW;
+  constexpr int OTH = POOL ? TH / 2 : TH;
+  constexpr int OPS = BN + 8;
+  constexpr int QN = BN / 8;
+  for (int it = tid; it < OTH * OTW * QN; it += 256) {
+    const int r = it / QN, q = it - r * QN;
+    const int oy = r / OTW, ox = r - oy * OTW;
+    int p;
+    if constexpr (POOL) {
+      p = oy * OTW + ox;
+    } else {
+      p = ((oy >> 1) * (TW / 2) + (ox >> 1)) * 4 + (oy & 1) * 2 + (ox & 1);
+    }
+    const u16x8 v = *(const u16x8*)(ostg + p * OPS + q * 8);
+    *(u16x8*)(out + (((size_t)b * Ho + oy0 + oy) * Wo + ox0 + ox) * Cout + n0 + q * 8) = v;
+  }
+}
+
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL>
+__global__ __launch_bounds__(256) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
+                                                       const uint16_t* __restrict__ wpk,
+                                                       const float* __restrict__ bias,
+                                                       uint16_t* __restrict__ out, int H, int W,
+                                                       int Cin, int Cout) {
+  constexpr int CK = CONV_CK, PS = CONV_PS;
+  constexpr int HH = TH + 2, HWD = TW + 2;
+  constexpr int NPIX = TH * TW;
+  constexpr int RT = ((NPIX + 15) / 16 + WM - 1) / WM * WM;
+  constexpr int RTW = RT / WM;
+  constexpr int CTW = BN / 16 / WN;
+  constexpr int HALO = HH * HWD * PS;
+  constexpr int WSL = BN * PS;
+  constexpr int OPIX = POOL ? NPIX / 4 : NPIX;
+  constexpr int OPS = BN + 8;
+  constexpr int OPER = 2 * HALO + 2 * WSL;
+  constexpr int OSTG = OPIX * OPS;
+  constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
+  constexpr int HITEMS = HH * HWD * 4;
+  constexpr int HLOADS = (HITEMS + 255) / 256;
+  constexpr int WITEMS = BN * 4;
+  constexpr int WLOADS = (WITEMS + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(TH % 2 == 0 && TW % 2 == 0, "window-major order needs even boxes");
+  static_assert(CTW * 16 * WN == BN, "BN split");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
+  const int b = blockIdx.x / tiles_per_img;
+  const int tile = blockIdx.x - b * tiles_per_img;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int nb = blockIdx.y;
+  const int nchunks = Cin / CK;
+  const int nsteps = nchunks * 9;
+  const uint16_t* in_b = in + (size_t)b * H * W * Cin;
+  const uint16_t* wblk = wpk + (size_t)nb * nchunks * 9 * BN * CK;
+
+  u16x8 hreg[HLOADS];
+  u16x8 wreg[WLOADS];
+
+  auto load_halo = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < HLOADS; ++i) {
+      const int it = tid + 256 * i;
+      u16x8 v = (u16x8)0;
+      if (it < HITEMS) {
+        const int p = it >> 2, q = it & 3;
+        const int hy = p / HWD, hx = p - (p / HWD) * HWD;
+        const int y = y0 + hy - 1, x = x0 + hx - 1;
+        if (y >= 0 && y < H && x >= 0 && x < W)
+          v = *(const u16x8*)(in_b + ((size_t)y * W + x) * Cin + c * CK + q * 8);
+      }
+      hreg[i] = v;
+    }
+  };
+  auto store_halo = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < HLOADS; ++i) {
+      const int it = tid + 256 * i;
+      if (it < HITEMS) *(u16x8*)(smem + buf * HALO + (it >> 2) * PS + (it & 3) * 8) = hreg[i];
+    }
+  };
+  auto load_w = [&](int s) {
+    const uint16_t* src = wblk + (size_t)s * BN * CK;
+#pragma unroll
+    for (int i = 0; i < WLOADS; ++i) {
+      const int it = tid + 256 * i;
+      if (it < WITEMS) wreg[i] = *(const u16x8*)(src + it * 8);
+    }
+  };
+  auto store_w = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < WLOADS; ++i) {
+      const int it = tid + 256 * i;
+      if (it < WITEMS) *(u16x8*)(smem + 2 * HALO + buf * WSL + (it >> 2) * PS + (it & 3) * 8) = wreg[i];
+    }
+  };
+
+  int abase[RTW];
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt) {
+    int m = (wm * RTW + rt) * 16 + (lane & 15);
+    if (m >= NPIX) m = 0;  // padding rows: computed on pixel 0, never stored
+    int py, px;
+    box_pixel<TW>(m, py, px);
+    abase[rt] = (py * HWD + px) * PS + (lane >> 4) * 8;
+  }
+  int bbase[CTW];
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) bbase[ct] = ((wn * CTW + ct) * 16 + (lane & 15)) * PS + (lane >> 4) * 8;
+
+  f32x4 acc[RTW][CTW];
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = (f32x4)0.f;
+
+  load_halo(0);
+  load_w(0);
+  store_halo(0);
+  store_w(0);
+  __syncthreads();
+
+  for (int s = 0; s < nsteps; ++s) {
+    const int c = s / 9, t = s - (s / 9) * 9;
+    const bool next_w = s + 1 < nsteps;
+    const bool next_h = c + 1 < nchunks;
+    if (next_w) load_w(s + 1);
+    if (t == 0 && next_h) load_halo(c + 1);
+    const int ky = t / 3, kx = t - (t / 3) * 3;
+    const uint16_t* hb = smem + (c & 1) * HALO + (ky * HWD + kx) * PS;
+    const uint16_t* wb = smem + 2 * HALO + (s & 1) * WSL;
+    u16x8 bfr[CTW];
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
+#pragma unroll
+    for (int rt = 0; rt < RTW; ++rt) {
+      const u16x8 a = *(const u16x8*)(hb + abase[rt]);
+#pragma unroll
+      for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(a, bfr[ct], acc[rt][ct]);
+    }
+    if (next_w) store_w((s + 1) & 1);
+    if (t == 8 && next_h) store_halo((c + 1) & 1);
+    __syncthreads();
+  }
+
+  // Epilogue: folded-BN bias + ReLU (+ 2x2 max) -> 16-bit -> LDS -> global.
+  uint16_t* ostg = smem;
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int nl = (wn * CTW + ct) * 16 + (lane & 15);
+    const float bv = bias[nb * BN + nl];
+#pragma unroll
+    for (int rt = 0; rt < RTW; ++rt) {
+      const f32x4 v = acc[rt][ct];
+      if constexpr (POOL) {
+        const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        const int w = (wm * RTW + rt) * 4 + (lane >> 4);
+        if (w < OPIX) ostg[w * OPS + nl] = T::from_f32(fmaxf(mx + bv, 0.f));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = (wm * RTW + rt) * 16 + (lane >> 4) * 4 + j;
+          if (m < NPIX) ostg[m * OPS + nl] = T::from_f32(fmaxf(v[j] + bv, 0.f));
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
+  const int oy0 = POOL ? y0 / 2 : y0, ox0 = POOL ? x0 / 2 : x0;
+  store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
+}
+
+// conv1 (3 -> 32 @224) with the input normalisation of cvit_prediction.py:
+// x/255 then (x - mean_c)/std_c (:41-42, :214-215), zero padding applied in
+// normalised space exactly like the reference's Conv2d(padding=1).
+// k = tap*4 + c (c padded to 4, taps padded to 16 -> K = 64 = two MFMA steps).
+// U8 = true: uint8 NHWC crops (the face-crop format, cvit_prediction.py:202);
+// U8 = false: already-normalised fp32 NCHW (CViT.forward's input contract).
+constexpr float kMean[3] = {0.485f, 0.456f, 0.406f};
+constexpr float kStd[3] = {0.229f, 0.224f, 0.225f};
+
+template <class T, bool U8>
+__global__ __launch_bounds__(256) void conv1_bn_relu(const void* __restrict__ in_,
+                                                     const uint16_t* __restrict__ w1,
+                                                     const float* __restrict__ bias,
+                                                     uint16_t* __restrict__ out, int H, int W) {
+  constexpr int TH = 16, TW = 16, HWD = 18, NH = 18 * 18, BN = 32;
+  constexpr int WPS = 64 + 8;
+  constexpr int OPS = BN + 8;
+  constexpr int HSZ = NH * 4;
+  constexpr int SMEM_OPER = HSZ + BN * WPS;
+  constexpr int SMEM_OUT = TH * TW * OPS;
+  constexpr int SMEM = SMEM_OPER > SMEM_OUT ? SMEM_OPER : SMEM_OUT;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+  uint16_t* halo = smem;
+  uint16_t* wl = smem + HSZ;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
+  const int b = blockIdx.x / tiles_per_img;
+  const int tile = blockIdx.x - b * tiles_per_img;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+
+  for (int p = tid; p < NH; p += 256) {
+    const int hy = p / HWD, hx = p - (p / HWD) * HWD;
+    const int y = y0 + hy - 1, x = x0 + hx - 1;
+    float v[3] = {0.f, 0.f, 0.f};
+    if (y >= 0 && y < H && x >= 0 && x < W) {
+      if constexpr (U8) {
+        const uint8_t* src = (const uint8_t*)in_ + (((size_t)b * H + y) * W + x) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = ((float)src[c] / 255.0f - kMean[c]) / kStd[c];
+      } else {
+        const float* src = (const float*)in_ + (size_t)b * 3 * H * W + (size_t)y * W + x;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = src[(size_t)c * H * W];
+      }
+    }
+    u16x4 h;
+    h[0] = T::from_f32(v[0]);
+    h[1] = T::from_f32(v[1]);
+    h[2] = T::from_f32(v[2]);
+    h[3] = 0;
+    *(u16x4*)(halo + p * 4) = h;
+  }
+  {
+    const int n = tid >> 3, q = tid & 7;
+    *(u16x8*)(wl + n * WPS + q * 8) = *(const u16x8*)(w1 + n * 64 + q * 8);
+  }
+  __syncthreads();
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt) acc[rt][0] = acc[rt][1] = (f32x4)0.f;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    u16x8 bfr[2];
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+      bfr[ct] = *(const u16x8*)(wl + (ct * 16 + (lane & 15)) * WPS + ks * 32 + (lane >> 4) * 8);
+    const int t0 = ks * 8 + (lane >> 4) * 2, t1 = t0 + 1;
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt) {
+      const int m = (wave * 4 + rt) * 16 + (lane & 15);
+      int py, px;
+      box_pixel<TW>(m, py, px);
+      u16x4 lo = (u16x4)0, hi = (u16x4)0;
+      if (t0 < 9) lo = *(const u16x4*)(halo + ((py + t0 / 3) * HWD + px + t0 % 3) * 4);
+      if (t1 < 9) hi = *(const u16x4*)(halo + ((py + t1 / 3) * HWD + px + t1 % 3) * 4);
+      const u16x8 a = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) acc[rt][ct] = T::mfma(a, bfr[ct], acc[rt][ct]);
+    }
+  }
+  __syncthreads();
+  uint16_t* ostg = smem;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int nl = ct * 16 + (lane & 15);
+    const float bv = bias[nl];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = (wave * 4 + rt) * 16 + (lane >> 4) * 4 + j;
+        ostg[m * OPS + nl] = T::from_f32(fmaxf(acc[rt][ct][j] + bv, 0.f));
+      }
+  }
+  __syncthreads();
+  store_tile<TH, TW, BN, false>(ostg, out, b, H, W, y0, x0, BN, 0, tid);
+}
+
+}  // namespace fac
+
+// ---------------------------------------------------------------------------
+// Host launchers (C++ linkage, used by cvit_abi.hip).
+namespace fac {
+
+// Per-resolution kernel configuration; must agree with conv_block_n() and
+// the weight packing in cvit_abi.hip.
+int conv_block_n(int H) { return H >= 112 ? (H == 224 ? 32 : 64) : 128; }
+
+template <class T>
+static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
+                                int B, int H, int W, int Cin, int Cout, bool pool, hipStream_t st) {
+  const int bn = conv_block_n(H);
+  if (H == 224 || H == 112) {
+    dim3 grid(B * (H / 16) * (W / 16), Cout / bn);
+    if (bn == 32) {
+      if (pool) conv3x3_bn_relu<T, 16, 16, 32, 4, 1, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
+      else conv3x3_bn_relu<T, 16, 16, 32, 4, 1, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
+    } else {
+      if (pool) conv3x3_bn_relu<T, 16, 16, 64, 4, 1, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
+      else conv3x3_bn_relu<T, 16, 16, 64, 4, 1, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
+    }
+  } else {
+    dim3 grid(B * (H / 14) * (W / 14), Cout / bn);
+    if (pool) conv3x3_bn_relu<T, 14, 14, 128, 2, 2, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
+    else conv3x3_bn_relu<T, 14, 14, 128, 2, 2, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
+                          int B, int H, int W, int Cin, int Cout, bool pool, hipStream_t st) {
+  if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, st);
+  return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, st);
+}
+
+hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
+                        int B, int H, int W, hipStream_t st) {
+  dim3 grid(B * (H / 16) * (W / 16));
+  if (dtype == 0) {
+    if (u8) conv1_bn_relu<BF16, true><<<grid, 256, 0, st>>>(in, w1, bias, out, H, W);
+    else conv1_bn_relu<BF16, false><<<grid, 256, 0, st>>>(in, w1, bias, out, H, W);
+  } else {
+    if (u8) conv1_bn_relu<F16, true><<<grid, 256, 0, st>>>(in, w1, bias, out, H, W);
+    else conv1_bn_relu<F16, false><<<grid, 256, 0, st>>>(in, w1, bias, out, H, W);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fac

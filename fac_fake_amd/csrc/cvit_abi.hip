@@ -1,0 +1,523 @@
+// C ABI (include/fac_cvit.h) and host orchestration of the CViT forward.
+//
+// Weight handling mirrors what the reference does implicitly at every call:
+// eval-mode BatchNorm2d (cvit.py:89..146) is folded into the preceding conv
+// once at load time (s = gamma / sqrt(var + eps); W' = W*s; b' = (b-mean)*s +
+// beta), conv weights are repacked into per-(n-block, 32-channel chunk, tap)
+// [BN][32] slices for the conv kernel, and linear weights are converted to
+// the 16-bit operand type.  LayerNorm params, the CLS/pos embeddings and the
+// final 2048->2 layer stay fp32.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/fac_cvit.h"
+#include "common.hpp"
+
+namespace fac {
+int conv_block_n(int H);
+hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
+                          int B, int H, int W, int Cin, int Cout, bool pool, hipStream_t st);
+hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
+                        int B, int H, int W, hipStream_t st);
+hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
+                       void* out, int ldo, int M, int N, int K, int splits, hipStream_t st);
+hipError_t launch_embed_finalize(const float* slab, int S, int B, const float* bias, const float* cls,
+                                 const float* pos, const int32_t* pidx, float* x, int* err, hipStream_t st);
+hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,
+                            hipStream_t st);
+hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipStream_t st);
+hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, float scale, hipStream_t st);
+hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, float* logits, float* probs, int B,
+                           hipStream_t st);
+hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st);
+enum { EPI_F32 = 0, EPI_F32_RELU = 1, EPI_T_GELU = 2, EPI_RESID = 3, EPI_PARTIAL = 4, EPI_T = 5 };
+}  // namespace fac
+
+namespace {
+
+constexpr int kDim = 1024, kDepth = 6, kMlp = 2048, kPatchDim = 25088, kImg = 224;
+constexpr float kBnEps = 1e-5f;
+
+const int kStem[17][2] = {{3, 32},    {32, 32},   {32, 32},   {32, 64},   {64, 64},   {64, 64},
+                          {64, 128},  {128, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256},
+                          {256, 256}, {256, 512}, {512, 512}, {512, 512}, {512, 512}};
+bool pool_after(int i) { return i == 2 || i == 5 || i == 8 || i == 12 || i == 16; }
+
+struct ConvLayer {
+  int H = 0, Cin = 0, Cout = 0;
+  bool pool = false;
+  uint16_t* w = nullptr;
+  float* b = nullptr;
+};
+
+struct TLayer {
+  float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
+  uint16_t *wqkv = nullptr, *wo = nullptr, *w1 = nullptr, *w2 = nullptr;
+  float *bo = nullptr, *b1 = nullptr, *b2 = nullptr;
+};
+
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DevGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+struct fac_ctx {
+  int device = 0;
+  int dtype = 0;
+  bool loaded = false;
+  std::string err;
+  std::vector<void*> weights;  // all weight allocations
+  uint16_t* conv1_w = nullptr;
+  float* conv1_b = nullptr;
+  ConvLayer conv[16];
+  uint16_t* pe_w = nullptr;
+  float *pe_b = nullptr, *cls = nullptr, *pos = nullptr;
+  TLayer tl[kDepth];
+  uint16_t* h1_w = nullptr;
+  float *h1_b = nullptr, *h2_w = nullptr, *h2_b = nullptr;
+  // workspace
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  int cap_B = 0;
+  int stem_chunk = 0;
+  uint16_t *act0 = nullptr, *act1 = nullptr, *stem_out = nullptr, *xn = nullptr, *o = nullptr, *hbuf = nullptr,
+           *cbuf = nullptr;
+  float *slab = nullptr, *x = nullptr, *qkv = nullptr, *hh = nullptr;
+  int* errflag = nullptr;
+};
+
+namespace {
+
+int set_err(fac_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                  \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return set_err(ctx, FAC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+uint16_t to16(int dtype, float f) { return dtype == 0 ? fac_host::f32_to_bf16(f) : fac_host::f32_to_f16(f); }
+
+int patch_splits(int B) { return B <= 64 ? 28 : 8; }
+
+struct WsLayout {
+  size_t act, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, total;
+};
+
+WsLayout layout(int B, int chunk) {
+  auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
+  WsLayout L{};
+  const int cb = (chunk > 0 && chunk < B) ? chunk : B;
+  const size_t S = (size_t)std::max(patch_splits(B) * std::min(B, 64), 8 * B);
+  size_t off = 0;
+  L.act = off; off += 2 * al((size_t)cb * kImg * kImg * 32 * 2);
+  L.stem = off; off += al((size_t)B * kPatchDim * 2);
+  L.slab = off; off += al(S * kDim * 4);
+  L.x = off; off += al((size_t)2 * B * kDim * 4);
+  L.xn = off; off += al((size_t)2 * B * kDim * 2);
+  L.qkv = off; off += al((size_t)2 * B * 3 * kDim * 4);
+  L.o = off; off += al((size_t)2 * B * kDim * 2);
+  L.hbuf = off; off += al((size_t)2 * B * kMlp * 2);
+  L.cbuf = off; off += al((size_t)B * kDim * 2);
+  L.hh = off; off += al((size_t)B * kMlp * 4);
+  L.err = off; off += 256;
+  L.total = off;
+  return L;
+}
+
+int ensure_ws(fac_ctx* c, int B) {
+  if (B <= c->cap_B && c->ws) return FAC_OK;
+  const WsLayout L = layout(B, c->stem_chunk);
+  if (c->ws) {
+    HIP_TRY(c, hipDeviceSynchronize());
+    HIP_TRY(c, hipFree(c->ws));
+    c->ws = nullptr;
+  }
+  if (hipMalloc(&c->ws, L.total) != hipSuccess) {
+    c->ws = nullptr;
+    c->cap_B = 0;
+    return set_err(c, FAC_ERR_OOM, "workspace allocation of " + std::to_string(L.total) + " bytes failed");
+  }
+  HIP_TRY(c, hipMemset(c->ws, 0, L.total));
+  char* base = (char*)c->ws;
+  const size_t half = (L.stem - L.act) / 2;
+  c->act0 = (uint16_t*)(base + L.act);
+  c->act1 = (uint16_t*)(base + L.act + half);
+  c->stem_out = (uint16_t*)(base + L.stem);
+  c->slab = (float*)(base + L.slab);
+  c->x = (float*)(base + L.x);
+  c->xn = (uint16_t*)(base + L.xn);
+  c->qkv = (float*)(base + L.qkv);
+  c->o = (uint16_t*)(base + L.o);
+  c->hbuf = (uint16_t*)(base + L.hbuf);
+  c->cbuf = (uint16_t*)(base + L.cbuf);
+  c->hh = (float*)(base + L.hh);
+  c->errflag = (int*)(base + L.err);
+  c->ws_bytes = L.total;
+  c->cap_B = B;
+  return FAC_OK;
+}
+
+template <class U>
+int upload(fac_ctx* c, const std::vector<U>& host, U** dst) {
+  void* p = nullptr;
+  if (hipMalloc(&p, host.size() * sizeof(U)) != hipSuccess) return set_err(c, FAC_ERR_OOM, "weight allocation failed");
+  c->weights.push_back(p);
+  HIP_TRY(c, hipMemcpy(p, host.data(), host.size() * sizeof(U), hipMemcpyHostToDevice));
+  *dst = (U*)p;
+  return FAC_OK;
+}
+
+struct Descs {
+  std::map<std::string, const fac_tensor_desc*> m;
+  fac_ctx* c;
+  std::string missing;
+  const float* get(const std::string& name, std::initializer_list<int64_t> shape, int* rc) {
+    auto it = m.find(name);
+    if (it == m.end()) {
+      *rc = set_err(c, FAC_ERR_MISSING, "missing state_dict key: " + name);
+      return nullptr;
+    }
+    const fac_tensor_desc* d = it->second;
+    std::vector<int64_t> want(shape);
+    bool ok = d->data != nullptr && d->ndim == (int)want.size();
+    for (size_t i = 0; ok && i < want.size(); ++i) ok = d->shape[i] == want[i];
+    if (!ok) {
+      std::string got;
+      for (int i = 0; i < d->ndim && i < 4; ++i) got += std::to_string(d->shape[i]) + ",";
+      *rc = set_err(c, FAC_ERR_SHAPE, "shape mismatch for " + name + " (got [" + got + "])");
+      return nullptr;
+    }
+    return d->data;
+  }
+};
+
+std::vector<uint16_t> convert16(int dtype, const float* src, size_t n) {
+  std::vector<uint16_t> out(n);
+  for (size_t i = 0; i < n; ++i) out[i] = to16(dtype, src[i]);
+  return out;
+}
+
+// nn.Sequential indices of conv i and its BatchNorm (cvit.py:86-148).
+void stem_indices(int i, int* cidx, int* bidx) {
+  int idx = 0;
+  for (int k = 0; k < i; ++k) idx += 3 + (pool_after(k) ? 1 : 0);
+  *cidx = idx;
+  *bidx = idx + 1;
+}
+
+int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
+  Descs D{{}, c, {}};
+  for (int i = 0; i < n; ++i) {
+    if (!descs[i].name) return set_err(c, FAC_ERR_ARG, "descriptor with null name");
+    D.m[descs[i].name] = &descs[i];
+  }
+  int rc = FAC_OK;
+#define GET(var, name, ...)                                 \
+  const float* var = D.get(name, {__VA_ARGS__}, &rc);       \
+  if (!var) return rc;
+
+  // ---- conv stem with BN folded
+  int H = kImg;
+  for (int i = 0; i < 17; ++i) {
+    const int ci = kStem[i][0], co = kStem[i][1];
+    int cidx, bidx;
+    stem_indices(i, &cidx, &bidx);
+    const std::string pc = "features." + std::to_string(cidx) + ".", pb = "features." + std::to_string(bidx) + ".";
+    GET(w, pc + "weight", co, ci, 3, 3);
+    GET(bconv, pc + "bias", co);
+    GET(gam, pb + "weight", co);
+    GET(bet, pb + "bias", co);
+    GET(mean, pb + "running_mean", co);
+    GET(var, pb + "running_var", co);
+    std::vector<float> s(co), bf(co);
+    for (int o = 0; o < co; ++o) {
+      s[o] = gam[o] / std::sqrt(var[o] + kBnEps);
+      bf[o] = (bconv[o] - mean[o]) * s[o] + bet[o];
+    }
+    auto wf = [&](int o, int cin, int t) { return w[((size_t)o * ci + cin) * 9 + t] * s[o]; };
+    if (i == 0) {
+      std::vector<uint16_t> pk((size_t)32 * 64, 0);
+      for (int o = 0; o < 32; ++o)
+        for (int t = 0; t < 9; ++t)
+          for (int cin = 0; cin < 3; ++cin) pk[(size_t)o * 64 + t * 4 + cin] = to16(c->dtype, wf(o, cin, t));
+      if ((rc = upload(c, pk, &c->conv1_w))) return rc;
+      if ((rc = upload(c, bf, &c->conv1_b))) return rc;
+    } else {
+      ConvLayer& L = c->conv[i - 1];
+      L.H = H;
+      L.Cin = ci;
+      L.Cout = co;
+      L.pool = pool_after(i);
+      const int BN = fac::conv_block_n(H), CK = 32, nch = ci / CK;
+      std::vector<uint16_t> pk((size_t)co * ci * 9);
+      size_t q = 0;
+      for (int nb = 0; nb < co / BN; ++nb)
+        for (int ch = 0; ch < nch; ++ch)
+          for (int t = 0; t < 9; ++t)
+            for (int nl = 0; nl < BN; ++nl)
+              for (int k = 0; k < CK; ++k) pk[q++] = to16(c->dtype, wf(nb * BN + nl, ch * CK + k, t));
+      if ((rc = upload(c, pk, &L.w))) return rc;
+      if ((rc = upload(c, bf, &L.b))) return rc;
+    }
+    if (pool_after(i)) H /= 2;
+  }
+
+  // ---- embeddings
+  GET(pos, "pos_embedding", 32, 1, kDim);
+  GET(cls, "cls_token", 1, 1, kDim);
+  GET(pew, "patch_to_embedding.weight", kDim, kPatchDim);
+  GET(peb, "patch_to_embedding.bias", kDim);
+  if ((rc = upload(c, std::vector<float>(pos, pos + 32 * kDim), &c->pos))) return rc;
+  if ((rc = upload(c, std::vector<float>(cls, cls + kDim), &c->cls))) return rc;
+  if ((rc = upload(c, convert16(c->dtype, pew, (size_t)kDim * kPatchDim), &c->pe_w))) return rc;
+  if ((rc = upload(c, std::vector<float>(peb, peb + kDim), &c->pe_b))) return rc;
+
+  // ---- transformer (cvit.py:64-78; key layout transformer.layers.{l}.{0,1}.fn.{norm,fn}.*)
+  for (int l = 0; l < kDepth; ++l) {
+    const std::string p = "transformer.layers." + std::to_string(l) + ".";
+    TLayer& T = c->tl[l];
+    GET(g1, p + "0.fn.norm.weight", kDim);
+    GET(b1n, p + "0.fn.norm.bias", kDim);
+    GET(wqkv, p + "0.fn.fn.to_qkv.weight", 3 * kDim, kDim);
+    GET(wo, p + "0.fn.fn.to_out.weight", kDim, kDim);
+    GET(bo, p + "0.fn.fn.to_out.bias", kDim);
+    GET(g2, p + "1.fn.norm.weight", kDim);
+    GET(b2n, p + "1.fn.norm.bias", kDim);
+    GET(w1, p + "1.fn.fn.net.0.weight", kMlp, kDim);
+    GET(b1, p + "1.fn.fn.net.0.bias", kMlp);
+    GET(w2, p + "1.fn.fn.net.2.weight", kDim, kMlp);
+    GET(b2, p + "1.fn.fn.net.2.bias", kDim);
+    if ((rc = upload(c, std::vector<float>(g1, g1 + kDim), &T.ln1_g))) return rc;
+    if ((rc = upload(c, std::vector<float>(b1n, b1n + kDim), &T.ln1_b))) return rc;
+    if ((rc = upload(c, std::vector<float>(g2, g2 + kDim), &T.ln2_g))) return rc;
+    if ((rc = upload(c, std::vector<float>(b2n, b2n + kDim), &T.ln2_b))) return rc;
+    if ((rc = upload(c, convert16(c->dtype, wqkv, (size_t)3 * kDim * kDim), &T.wqkv))) return rc;
+    if ((rc = upload(c, convert16(c->dtype, wo, (size_t)kDim * kDim), &T.wo))) return rc;
+    if ((rc = upload(c, std::vector<float>(bo, bo + kDim), &T.bo))) return rc;
+    if ((rc = upload(c, convert16(c->dtype, w1, (size_t)kMlp * kDim), &T.w1))) return rc;
+    if ((rc = upload(c, std::vector<float>(b1, b1 + kMlp), &T.b1))) return rc;
+    if ((rc = upload(c, convert16(c->dtype, w2, (size_t)kDim * kMlp), &T.w2))) return rc;
+    if ((rc = upload(c, std::vector<float>(b2, b2 + kDim), &T.b2))) return rc;
+  }
+
+  // ---- head (cvit.py:161-165)
+  GET(h1w, "mlp_head.0.weight", kMlp, kDim);
+  GET(h1b, "mlp_head.0.bias", kMlp);
+  GET(h2w, "mlp_head.2.weight", 2, kMlp);
+  GET(h2b, "mlp_head.2.bias", 2);
+  if ((rc = upload(c, convert16(c->dtype, h1w, (size_t)kMlp * kDim), &c->h1_w))) return rc;
+  if ((rc = upload(c, std::vector<float>(h1b, h1b + kMlp), &c->h1_b))) return rc;
+  if ((rc = upload(c, std::vector<float>(h2w, h2w + 2 * kMlp), &c->h2_w))) return rc;
+  if ((rc = upload(c, std::vector<float>(h2b, h2b + 2), &c->h2_b))) return rc;
+#undef GET
+  c->loaded = true;
+  return FAC_OK;
+}
+
+// Optional per-stage event timing (fac_profile_forward_u8) and early exit
+// after conv `stop_after` (fac_debug_features_u8, -1 = full forward).
+struct Prof {
+  hipEvent_t ev[24];
+  int n = 0;
+};
+
+int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
+                 void* stream, Prof* prof = nullptr, int stop_after = -1, uint16_t* feat_out = nullptr) {
+  using namespace fac;
+  if (!c) return FAC_ERR_ARG;
+  if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "forward before fac_load_weights");
+  if (B <= 0 || !in || (stop_after < 0 && (!pidx || !logits))) return set_err(c, FAC_ERR_ARG, "bad forward arguments");
+  DevGuard g(c->device);
+  int rc = ensure_ws(c, B);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const int dt = c->dtype;
+  const int chunk = (c->stem_chunk > 0 && c->stem_chunk < B && !prof && stop_after < 0) ? c->stem_chunk : B;
+#define MARK()                                                       \
+  do {                                                               \
+    if (prof) HIP_TRY(c, hipEventRecord(prof->ev[prof->n++], st));  \
+  } while (0)
+  MARK();
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nb = std::min(chunk, B - b0);
+    const void* src = u8 ? (const void*)((const uint8_t*)in + (size_t)b0 * kImg * kImg * 3)
+                         : (const void*)((const float*)in + (size_t)b0 * 3 * kImg * kImg);
+    HIP_TRY(c, launch_conv1(dt, u8, src, c->conv1_w, c->conv1_b, c->act0, nb, kImg, kImg, st));
+    MARK();
+    uint16_t *cur = c->act0, *nxt = c->act1;
+    if (stop_after == 0) {
+      HIP_TRY(c, hipMemcpyAsync(feat_out, cur, (size_t)nb * kImg * kImg * 32 * 2, hipMemcpyDeviceToDevice, st));
+      return FAC_OK;
+    }
+    for (int l = 0; l < 16; ++l) {
+      const ConvLayer& L = c->conv[l];
+      uint16_t* dst = (l == 15) ? c->stem_out + (size_t)b0 * kPatchDim : nxt;
+      HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, nb, L.H, L.H, L.Cin, L.Cout, L.pool, st));
+      MARK();
+      if (stop_after == l + 1) {
+        const int Ho = L.pool ? L.H / 2 : L.H;
+        HIP_TRY(c, hipMemcpyAsync(feat_out, dst, (size_t)nb * Ho * Ho * L.Cout * 2, hipMemcpyDeviceToDevice, st));
+        return FAC_OK;
+      }
+      std::swap(cur, nxt);
+    }
+  }
+  const int S = patch_splits(B);
+  HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->stem_out, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
+                         kPatchDim, S, st));
+  HIP_TRY(c, launch_embed_finalize(c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->errflag, st));
+  MARK();
+  const int R = 2 * B;
+  const float scale = 1.0f / std::sqrt((float)kDim);  // dim ** -0.5 (cvit.py:38), not head_dim
+  for (int l = 0; l < kDepth; ++l) {
+    const TLayer& T = c->tl[l];
+    HIP_TRY(c, launch_layernorm(dt, c->x, T.ln1_g, T.ln1_b, c->xn, R, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st));
+    HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_RESID, c->o, kDim, T.wo, kDim, T.bo, c->x, kDim, R, kDim, kDim, 1, st));
+    HIP_TRY(c, launch_layernorm(dt, c->x, T.ln2_g, T.ln2_b, c->xn, R, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_RESID, c->hbuf, kMlp, T.w2, kMlp, T.b2, c->x, kDim, R, kDim, kMlp, 1, st));
+  }
+  MARK();
+  HIP_TRY(c, launch_gather_cls(dt, c->x, c->cbuf, B, st));
+  HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, c->hh, kMlp, B, kMlp, kDim, 1, st));
+  HIP_TRY(c, launch_head_out(c->hh, c->h2_w, c->h2_b, logits, probs, B, st));
+  MARK();
+#undef MARK
+  return FAC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fac_create(int device, int dtype, fac_ctx** out) {
+  if (!out || (dtype != FAC_DTYPE_BF16 && dtype != FAC_DTYPE_F16)) return FAC_ERR_ARG;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return FAC_ERR_HIP;
+  fac_ctx* c = new fac_ctx();
+  c->device = device;
+  c->dtype = dtype;
+  *out = c;
+  return FAC_OK;
+}
+
+int fac_load_weights(fac_ctx* c, const fac_tensor_desc* descs, int n) {
+  if (!c || !descs || n <= 0) return set_err(c, FAC_ERR_ARG, "bad load arguments");
+  DevGuard g(c->device);
+  for (void* p : c->weights) (void)hipFree(p);
+  c->weights.clear();
+  c->loaded = false;
+  return load_impl(c, descs, n);
+}
+
+int fac_reserve(fac_ctx* c, int max_batch) {
+  if (!c || max_batch <= 0) return set_err(c, FAC_ERR_ARG, "bad reserve arguments");
+  DevGuard g(c->device);
+  return ensure_ws(c, max_batch);
+}
+
+int fac_workspace_bytes(fac_ctx* c, int B, size_t* out) {
+  if (!c || !out || B <= 0) return FAC_ERR_ARG;
+  *out = layout(B, c->stem_chunk).total;
+  return FAC_OK;
+}
+
+int fac_set_stem_chunk(fac_ctx* c, int crops) {
+  if (!c || crops < 0) return FAC_ERR_ARG;
+  if (crops != c->stem_chunk) {
+    c->stem_chunk = crops;
+    const int cap = c->cap_B;
+    c->cap_B = 0;  // force re-layout on next use
+    if (cap > 0) {
+      DevGuard g(c->device);
+      return ensure_ws(c, cap);
+    }
+  }
+  return FAC_OK;
+}
+
+int fac_forward_nchw_f32(fac_ctx* c, const float* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,
+                         void* stream) {
+  return forward_impl(c, d_in, false, B, d_pos, d_logits, d_probs, stream);
+}
+
+int fac_forward_nhwc_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,
+                        void* stream) {
+  return forward_impl(c, d_in, true, B, d_pos, d_logits, d_probs, stream);
+}
+
+int fac_debug_features_u8(fac_ctx* c, const uint8_t* d_in, int B, int layer, uint16_t* d_out, void* stream) {
+  if (!c || !d_out || layer < 0 || layer > 16) return set_err(c, FAC_ERR_ARG, "bad debug_features arguments");
+  return forward_impl(c, d_in, true, B, nullptr, nullptr, nullptr, stream, nullptr, layer, d_out);
+}
+
+int fac_profile_forward_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits,
+                           float* stage_ms, int n_stages, void* stream) {
+  if (!c || !stage_ms || n_stages < FAC_PROFILE_STAGES) return set_err(c, FAC_ERR_ARG, "bad profile arguments");
+  DevGuard g(c->device);
+  Prof p;
+  for (int i = 0; i <= FAC_PROFILE_STAGES; ++i) HIP_TRY(c, hipEventCreate(&p.ev[i]));
+  int rc = forward_impl(c, d_in, true, B, d_pos, d_logits, nullptr, stream, &p);
+  if (rc == FAC_OK) {
+    HIP_TRY(c, hipEventSynchronize(p.ev[p.n - 1]));
+    for (int i = 0; i + 1 < p.n && i < FAC_PROFILE_STAGES; ++i) HIP_TRY(c, hipEventElapsedTime(&stage_ms[i], p.ev[i], p.ev[i + 1]));
+  }
+  for (int i = 0; i <= FAC_PROFILE_STAGES; ++i) (void)hipEventDestroy(p.ev[i]);
+  return rc;
+}
+
+int fac_check_device_errors(fac_ctx* c, int* flags) {
+  if (!c || !flags) return FAC_ERR_ARG;
+  *flags = 0;
+  if (!c->errflag) return FAC_OK;
+  DevGuard g(c->device);
+  HIP_TRY(c, hipDeviceSynchronize());
+  HIP_TRY(c, hipMemcpy(flags, c->errflag, sizeof(int), hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemset(c->errflag, 0, sizeof(int)));
+  return FAC_OK;
+}
+
+int fac_video_score(const float* d_logits, int n, float* d_score, void* stream) {
+  if (!d_score || n < 0 || (n > 0 && !d_logits)) return FAC_ERR_ARG;
+  return fac::launch_video_score(d_logits, n, d_score, (hipStream_t)stream) == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+const char* fac_last_error(fac_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void fac_destroy(fac_ctx* c) {
+  if (!c) return;
+  {
+    DevGuard g(c->device);
+    (void)hipDeviceSynchronize();
+    for (void* p : c->weights) (void)hipFree(p);
+    if (c->ws) (void)hipFree(c->ws);
+  }
+  delete c;
+}
+
+const char* fac_version(void) { return "fac_cvit 0.1.0 (gfx950, MFMA 16x16x32 bf16/f16)"; }
+
+}  // extern "C"

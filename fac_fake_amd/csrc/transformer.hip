@@ -1,0 +1,358 @@
+// Patch embedding, transformer encoder and head of CViT
+// (CViT-main/model/cvit.py:5-78 and :150-179) on gfx950.
+//
+// Token layout: the residual stream is fp32 [2B][1024], row 2b = CLS token of
+// crop b, row 2b+1 = its single patch token (num_patches = (7//7)^2 = 1,
+// cvit.py:150).  Linear layers run as 16-bit x 16-bit MFMA GEMMs
+// (C = A[M][K] * W[N][K]^T) with fp32 accumulation and fused epilogues:
+// bias, exact-erf GELU, ReLU, fp32 residual add, or split-K fp32 partials.
+#include "common.hpp"
+
+namespace fac {
+
+enum GemmEpi : int {
+  EPI_F32 = 0,        // out f32 = acc + bias
+  EPI_F32_RELU = 1,   // out f32 = relu(acc + bias)
+  EPI_T_GELU = 2,     // out T = gelu(acc + bias)
+  EPI_RESID = 3,      // out f32 += acc + bias   (Residual, cvit.py:10-11)
+  EPI_PARTIAL = 4,    // out f32 [z][M][N] = acc (split-K slab)
+  EPI_T = 5,          // out T = acc + bias
+};
+
+// 64x64 output tile, BK = 64, 4 waves in a 2x2 grid (32x32 each = 2x2 MFMA
+// 16x16x32 tiles), register-staged double-buffered LDS.
+template <class T, int EPI>
+__global__ __launch_bounds__(256) void gemm_nt(const uint16_t* __restrict__ A, int lda,
+                                               const uint16_t* __restrict__ Wt, int ldw,
+                                               const float* __restrict__ bias, void* __restrict__ out_,
+                                               int ldo, int M, int N, int Kper) {
+  constexpr int BM = 64, BN = 64, BK = 64, PS = BK + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (BM + BN) * PS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int k0 = blockIdx.z * Kper;
+  const int nkt = Kper / BK;
+
+  u16x8 ra[2], rb[2];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int it = tid + 256 * i;
+      const int r = it >> 3, q = it & 7;
+      const int m = m0 + r;
+      ra[i] = (m < M) ? *(const u16x8*)(A + (size_t)m * lda + k0 + kt * BK + q * 8) : (u16x8)0;
+      rb[i] = *(const u16x8*)(Wt + (size_t)(n0 + r) * ldw + k0 + kt * BK + q * 8);
+    }
+  };
+  auto store = [&](int buf) {
+    uint16_t* sa = smem + buf * (BM + BN) * PS;
+    uint16_t* sb = sa + BM * PS;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int it = tid + 256 * i;
+      const int r = it >> 3, q = it & 7;
+      *(u16x8*)(sa + r * PS + q * 8) = ra[i];
+      *(u16x8*)(sb + r * PS + q * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = (f32x4)0.f;
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) load(kt + 1);
+    const uint16_t* sa = smem + (kt & 1) * (BM + BN) * PS;
+    const uint16_t* sb = sa + BM * PS;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      u16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        af[i] = *(const u16x8*)(sa + (wm * 32 + i * 16 + (lane & 15)) * PS + ks * 32 + (lane >> 4) * 8);
+        bfr[i] = *(const u16x8*)(sb + (wn * 32 + i * 16 + (lane & 15)) * PS + ks * 32 + (lane >> 4) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
+    }
+    if (kt + 1 < nkt) store((kt + 1) & 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+    const float bv = (EPI == EPI_PARTIAL || bias == nullptr) ? 0.f : bias[n];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (m >= M) continue;
+        const float v = acc[i][j][r] + bv;
+        if constexpr (EPI == EPI_F32) {
+          ((float*)out_)[(size_t)m * ldo + n] = v;
+        } else if constexpr (EPI == EPI_F32_RELU) {
+          ((float*)out_)[(size_t)m * ldo + n] = fmaxf(v, 0.f);
+        } else if constexpr (EPI == EPI_T_GELU) {
+          const float g = 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
+          ((uint16_t*)out_)[(size_t)m * ldo + n] = T::from_f32(g);
+        } else if constexpr (EPI == EPI_RESID) {
+          ((float*)out_)[(size_t)m * ldo + n] += v;
+        } else if constexpr (EPI == EPI_PARTIAL) {
+          ((float*)out_)[((size_t)blockIdx.z * M + m) * ldo + n] = v;
+        } else {
+          ((uint16_t*)out_)[(size_t)m * ldo + n] = T::from_f32(v);
+        }
+      }
+  }
+}
+
+// x[2b] = cls + pos[p_b];  x[2b+1] = (sum_s slab[s][b]) + bias + pos[p_b]
+// (cvit.py:171-175: patch_to_embedding, cat(cls, y), += pos_embedding[0:B],
+// with pos indexed by the crop's batch slot p_b).
+__global__ __launch_bounds__(256) void embed_finalize(const float* __restrict__ slab, int S, int B,
+                                                      const float* __restrict__ bias,
+                                                      const float* __restrict__ cls,
+                                                      const float* __restrict__ pos,
+                                                      const int32_t* __restrict__ pidx, float* __restrict__ x,
+                                                      int* __restrict__ err) {
+  const int b = blockIdx.x;
+  int p = pidx[b];
+  if (p < 0 || p >= 32) {
+    if (threadIdx.x == 0) atomicOr(err, 1);
+    p = p < 0 ? 0 : 31;
+  }
+  for (int n = threadIdx.x; n < 1024; n += 256) {
+    float y = 0.f;
+    for (int s = 0; s < S; ++s) y += slab[((size_t)s * B + b) * 1024 + n];
+    const float pe = pos[p * 1024 + n];
+    x[(size_t)(2 * b) * 1024 + n] = cls[n] + pe;
+    x[(size_t)(2 * b + 1) * 1024 + n] = (y + bias[n]) + pe;
+  }
+}
+
+// LayerNorm(1024, eps 1e-5) (PreNorm, cvit.py:13-20): one wave per row,
+// fp32 statistics, 16-bit output feeding the next GEMM.  With `stride2` the
+// kernel reads only rows 0, 2, 4... (the CLS rows) and skips the affine.
+template <class T>
+__global__ __launch_bounds__(256) void layernorm_rows(const float* __restrict__ x, const float* __restrict__ g,
+                                                      const float* __restrict__ bta, uint16_t* __restrict__ y,
+                                                      int R) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  const float* xr = x + (size_t)row * 1024;
+  f32x4 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = *(const f32x4*)(xr + i * 256 + lane * 4);
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mean = wave_sum(s) * (1.0f / 1024.0f);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = v[i][j] - mean;
+      q += d * d;
+    }
+  const float var = wave_sum(q) * (1.0f / 1024.0f);
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = i * 256 + lane * 4;
+    u16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = T::from_f32((v[i][j] - mean) * rstd * g[c + j] + bta[c + j]);
+    *(u16x4*)(y + (size_t)row * 1024 + c) = o;
+  }
+}
+
+// CLS rows of the fp32 residual stream -> 16-bit [B][1024] (cvit.py:177).
+template <class T>
+__global__ __launch_bounds__(256) void gather_cls(const float* __restrict__ x, uint16_t* __restrict__ c, int B) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over B*256 float4 groups
+  if (i >= B * 256) return;
+  const int b = i >> 8, q = i & 255;
+  const f32x4 v = *(const f32x4*)(x + (size_t)(2 * b) * 1024 + q * 4);
+  u16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = T::from_f32(v[j]);
+  *(u16x4*)(c + (size_t)b * 1024 + q * 4) = o;
+}
+
+// Attention core for n = 2 tokens, 8 heads x 128 (cvit.py:43-60):
+// dots = q.k^T * dim^-0.5 (dim = 1024, so 1/32), softmax over keys, out = attn.v.
+// One wave per (crop, head); qkv is fp32 [2B][3072] laid out '(qkv h d)'.
+template <class T>
+__global__ __launch_bounds__(256) void attention2(const float* __restrict__ qkv, uint16_t* __restrict__ o,
+                                                  int B, float scale) {
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (wid >= B * 8) return;
+  const int b = wid >> 3, h = wid & 7;
+  const float* r0 = qkv + (size_t)(2 * b) * 3072 + h * 128;
+  const float* r1 = r0 + 3072;
+  float q0[2], q1[2], k0[2], k1[2], v0[2], v1[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d = lane + 64 * i;
+    q0[i] = r0[d];
+    k0[i] = r0[1024 + d];
+    v0[i] = r0[2048 + d];
+    q1[i] = r1[d];
+    k1[i] = r1[1024 + d];
+    v1[i] = r1[2048 + d];
+  }
+  float s00 = 0.f, s01 = 0.f, s10 = 0.f, s11 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    s00 += q0[i] * k0[i];
+    s01 += q0[i] * k1[i];
+    s10 += q1[i] * k0[i];
+    s11 += q1[i] * k1[i];
+  }
+  s00 = wave_sum(s00) * scale;
+  s01 = wave_sum(s01) * scale;
+  s10 = wave_sum(s10) * scale;
+  s11 = wave_sum(s11) * scale;
+  const float m0 = fmaxf(s00, s01), m1 = fmaxf(s10, s11);
+  const float e00 = expf(s00 - m0), e01 = expf(s01 - m0);
+  const float e10 = expf(s10 - m1), e11 = expf(s11 - m1);
+  const float a00 = e00 / (e00 + e01), a01 = e01 / (e00 + e01);
+  const float a10 = e10 / (e10 + e11), a11 = e11 / (e10 + e11);
+  uint16_t* o0 = o + (size_t)(2 * b) * 1024 + h * 128;
+  uint16_t* o1 = o0 + 1024;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d = lane + 64 * i;
+    o0[d] = T::from_f32(a00 * v0[i] + a01 * v1[i]);
+    o1[d] = T::from_f32(a10 * v0[i] + a11 * v1[i]);
+  }
+}
+
+// Final Linear(2048 -> 2) + per-logit sigmoid (cvit.py:164, pred_sig in
+// cvit_prediction.py:258-259); fp32 weights and activations.  One wave per crop.
+__global__ __launch_bounds__(256) void head_out(const float* __restrict__ hid, const float* __restrict__ w2,
+                                                const float* __restrict__ b2, float* __restrict__ logits,
+                                                float* __restrict__ probs, int B) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const float* hr = hid + (size_t)b * 2048;
+  float s0 = 0.f, s1 = 0.f;
+  for (int k = lane * 4; k < 2048; k += 256) {
+    const f32x4 h = *(const f32x4*)(hr + k);
+    const f32x4 a = *(const f32x4*)(w2 + k);
+    const f32x4 c = *(const f32x4*)(w2 + 2048 + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s0 += h[j] * a[j];
+      s1 += h[j] * c[j];
+    }
+  }
+  s0 = wave_sum(s0) + b2[0];
+  s1 = wave_sum(s1) + b2[1];
+  if (lane == 0) {
+    logits[2 * b] = s0;
+    logits[2 * b + 1] = s1;
+    if (probs) {
+      probs[2 * b] = 1.0f / (1.0f + expf(-s0));
+      probs[2 * b + 1] = 1.0f / (1.0f + expf(-s1));
+    }
+  }
+}
+
+// Video-level score (pre_process_prediction, cvit_prediction.py:266-281) over
+// n per-crop logit pairs: p = sigmoid(logits); if n > 2: f = mean p0,
+// r = mean p1, score = f if f > r else |1 - r|; else 0.5.  Sequential fp32
+// sums in crop order (the reference's Python sum() over 0-d tensors).
+__global__ void video_score(const float* __restrict__ logits, int n, float* __restrict__ score) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (n <= 2) {
+    *score = 0.5f;
+    return;
+  }
+  float f = 0.f, r = 0.f;
+  for (int i = 0; i < n; ++i) {
+    f += 1.0f / (1.0f + expf(-logits[2 * i]));
+    r += 1.0f / (1.0f + expf(-logits[2 * i + 1]));
+  }
+  f = f / (float)n;
+  r = r / (float)n;
+  *score = f > r ? f : fabsf(1.0f - r);
+}
+
+}  // namespace fac
+
+namespace fac {
+
+template <class T>
+static hipError_t launch_gemm_t(int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
+                                void* out, int ldo, int M, int N, int K, int splits, hipStream_t st) {
+  dim3 grid(N / 64, (M + 63) / 64, splits);
+  const int Kper = K / splits;
+  switch (epi) {
+    case EPI_F32: gemm_nt<T, EPI_F32><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case EPI_F32_RELU: gemm_nt<T, EPI_F32_RELU><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case EPI_T_GELU: gemm_nt<T, EPI_T_GELU><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case EPI_RESID: gemm_nt<T, EPI_RESID><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case EPI_PARTIAL: gemm_nt<T, EPI_PARTIAL><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    default: gemm_nt<T, EPI_T><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
+                       void* out, int ldo, int M, int N, int K, int splits, hipStream_t st) {
+  if (N % 64 != 0 || K % (64 * splits) != 0) return hipErrorInvalidValue;
+  if (dtype == 0) return launch_gemm_t<BF16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, st);
+  return launch_gemm_t<F16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, st);
+}
+
+hipError_t launch_embed_finalize(const float* slab, int S, int B, const float* bias, const float* cls,
+                                 const float* pos, const int32_t* pidx, float* x, int* err, hipStream_t st) {
+  embed_finalize<<<B, 256, 0, st>>>(slab, S, B, bias, cls, pos, pidx, x, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,
+                            hipStream_t st) {
+  dim3 grid((R + 3) / 4);
+  if (dtype == 0) layernorm_rows<BF16><<<grid, 256, 0, st>>>(x, g, b, y, R);
+  else layernorm_rows<F16><<<grid, 256, 0, st>>>(x, g, b, y, R);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipStream_t st) {
+  dim3 grid(B);
+  if (dtype == 0) gather_cls<BF16><<<grid, 256, 0, st>>>(x, c, B);
+  else gather_cls<F16><<<grid, 256, 0, st>>>(x, c, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, float scale, hipStream_t st) {
+  dim3 grid((B * 8 + 3) / 4);
+  if (dtype == 0) attention2<BF16><<<grid, 256, 0, st>>>(qkv, o, B, scale);
+  else attention2<F16><<<grid, 256, 0, st>>>(qkv, o, B, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, float* logits, float* probs, int B,
+                           hipStream_t st) {
+  head_out<<<(B + 3) / 4, 256, 0, st>>>(hid, w2, b2, logits, probs, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st) {
+  video_score<<<1, 64, 0, st>>>(logits, n, score);
+  return hipGetLastError();
+}
+
+}  // namespace fac

@@ -1,0 +1,207 @@
+"""Drop-in ``CViT`` for the reference's inference path, running on gfx950 HIP kernels.
+
+Interface parity with ``CViT-main/model/cvit.py``:
+
+* constructor ``CViT(image_size=224, patch_size=7, num_classes=2, channels=512,
+  dim=1024, depth=6, heads=8, mlp_dim=2048)`` (cvit.py:81-82);
+* ``state_dict()`` / ``load_state_dict()`` with the same 193 keys, shapes and
+  order (checkpoints written by ``cvit_train.py:210`` load unchanged);
+* ``forward(img, mask=None)`` on normalised fp32 NCHW ``[B,3,224,224]``
+  returning fp32 logits ``[B,2]`` (cvit.py:167-179), including the
+  reference's batch-slot ``pos_embedding`` rule (crop j of a call gets
+  ``pos_embedding[j]``, cvit.py:174-175) and its ``B > 32`` RuntimeError.
+
+The parameters live in a tree of plain containers purely to expose the
+reference's state_dict; the arithmetic never runs through them.  On the first
+forward after (re)loading, the state_dict is handed to ``fac_load_weights``
+(BN folding + 16-bit repacking in C++), and every forward is one call into
+``libfac_cvit.so`` on the current torch stream.  There is no CPU fallback:
+a CPU tensor or a missing library raises.
+
+Extensions beyond the reference: ``pos_index=`` (explicit slot per crop, for
+sharded / chunked calls), ``forward_u8()`` taking raw uint8 NHWC face crops
+with the normalisation fused into conv1, and ``dtype`` ("bf16" or "fp16": the
+16-bit MFMA operand type; accumulation is fp32 either way).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+from torch import nn
+
+from . import _lib
+from .weights import cvit_param_specs
+
+SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
+                 mlp_dim=2048)
+MAX_SLOTS = 32  # pos_embedding has 32 rows (cvit.py:154)
+_BUFFER_KINDS = ("rmean", "rvar", "nbt")
+
+
+class _Node(nn.Module):
+    """Parameter container (keeps state_dict paths such as features.1.running_var)."""
+
+    def forward(self, *a, **k):  # pragma: no cover - never called
+        raise RuntimeError("parameter container")
+
+
+def _init_tensor(shape, kind):
+    if kind == "nbt":
+        return torch.zeros((), dtype=torch.long)
+    if kind in ("rmean", "beta", "cbias", "lbias"):
+        return torch.zeros(shape)
+    if kind in ("rvar", "gamma"):
+        return torch.ones(shape)
+    if kind == "emb":
+        return torch.randn(shape)
+    t = torch.empty(shape)
+    fan_in = int(math.prod(shape[1:]))
+    bound = 1.0 / math.sqrt(fan_in)
+    return t.uniform_(-bound, bound)
+
+
+class CViT(nn.Module):
+    def __init__(self, image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
+                 mlp_dim=2048, *, dtype: str = "bf16"):
+        super().__init__()
+        assert image_size % patch_size == 0, "image dimensions must be divisible by the patch size"
+        cfg = dict(image_size=image_size, patch_size=patch_size, num_classes=num_classes, channels=channels, dim=dim,
+                   depth=depth, heads=heads, mlp_dim=mlp_dim)
+        if cfg != SUPPORTED:
+            raise NotImplementedError(f"the gfx950 CViT path implements the cvit_prediction.py configuration "
+                                      f"{SUPPORTED}, got {cfg}")
+        if dtype not in _lib.DTYPES:
+            raise ValueError(f"dtype must be one of {list(_lib.DTYPES)}")
+        self.patch_size = patch_size
+        self.dtype_name = dtype
+        for name, shape, kind in cvit_param_specs(dim=dim, depth=depth, mlp_dim=mlp_dim, num_classes=num_classes,
+                                                  channels=channels, patch_size=patch_size):
+            *path, leaf = name.split(".")
+            mod = self
+            for p in path:
+                if p not in mod._modules:
+                    mod.add_module(p, _Node())
+                mod = mod._modules[p]
+            t = _init_tensor(shape, kind)
+            if kind in _BUFFER_KINDS:
+                mod.register_buffer(leaf, t)
+            else:
+                mod.register_parameter(leaf, nn.Parameter(t))
+        self._ctx = None
+        self._ctx_device = None
+        self._loaded_versions = None
+        self.eval()
+
+    # ------------------------------------------------------------------ weights
+    def _versions(self):
+        return tuple(t._version for t in self.state_dict(keep_vars=True).values()) + (
+            tuple(t.data_ptr() for t in self.parameters()),)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._loaded_versions = None
+        return out
+
+    def _ensure_ctx(self, device: torch.device):
+        lib = _lib.load()
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        if self._ctx is None or self._ctx_device != idx:
+            self._release()
+            h = ctypes.c_void_p()
+            _lib.check(lib.fac_create(idx, _lib.DTYPES[self.dtype_name], ctypes.byref(h)), None, "fac_create")
+            self._ctx, self._ctx_device, self._loaded_versions = h, idx, None
+        v = self._versions()
+        if self._loaded_versions != v:
+            keep, descs = [], []
+            for k, t in self.state_dict().items():
+                if k.endswith("num_batches_tracked"):
+                    continue
+                h = t.detach().to("cpu", torch.float32).contiguous()
+                keep.append(h)
+                d = _lib.TensorDesc()
+                d.name = k.encode()
+                d.data = h.data_ptr()
+                d.ndim = h.dim()
+                for i, s in enumerate(h.shape):
+                    d.shape[i] = s
+                descs.append(d)
+            arr = (_lib.TensorDesc * len(descs))(*descs)
+            _lib.check(lib.fac_load_weights(self._ctx, ctypes.cast(arr, ctypes.c_void_p), len(descs)), self._ctx,
+                       "fac_load_weights")
+            self._loaded_versions = v
+        return lib
+
+    def reserve(self, max_batch: int, device=None):
+        """Pre-size the device workspace (call before CUDA-graph capture)."""
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        lib = self._ensure_ctx(dev)
+        _lib.check(lib.fac_reserve(self._ctx, int(max_batch)), self._ctx, "fac_reserve")
+
+    def set_stem_chunk(self, crops: int):
+        if self._ctx is None:
+            raise RuntimeError("no device context yet: call reserve() or forward() first")
+        _lib.check(_lib.load().fac_set_stem_chunk(self._ctx, int(crops)), self._ctx, "fac_set_stem_chunk")
+
+    def _release(self):
+        if self._ctx is not None:
+            _lib.load().fac_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise RuntimeError("the gfx950 CViT path is inference-only (eval-mode BatchNorm is folded into the convs)")
+        return super().train(False)
+
+    # ------------------------------------------------------------------ forward
+    @staticmethod
+    def _pos_index(B: int, pos_index, device) -> torch.Tensor:
+        if pos_index is None:
+            if B > MAX_SLOTS:
+                # what `x += self.pos_embedding[0:B]` raises in the reference (cvit.py:175)
+                raise RuntimeError(f"The size of tensor a ({B}) must match the size of tensor b ({MAX_SLOTS}) "
+                                   f"at non-singleton dimension 0")
+            return torch.arange(B, dtype=torch.int32, device=device)
+        p = torch.as_tensor(pos_index)
+        if p.shape != (B,):
+            raise ValueError(f"pos_index must have shape ({B},), got {tuple(p.shape)}")
+        if p.numel() and (int(p.min()) < 0 or int(p.max()) >= MAX_SLOTS):
+            raise IndexError(f"pos_index values must lie in [0, {MAX_SLOTS})")
+        return p.to(device=device, dtype=torch.int32).contiguous()
+
+    def _run(self, x, B, pos_index, u8: bool, want_probs: bool):
+        if not x.is_cuda:
+            raise RuntimeError("CViT (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
+        lib = self._ensure_ctx(x.device)
+        pidx = self._pos_index(B, pos_index, x.device)
+        logits = torch.empty(B, 2, dtype=torch.float32, device=x.device)
+        probs = torch.empty(B, 2, dtype=torch.float32, device=x.device) if want_probs else None
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        fn = lib.fac_forward_nhwc_u8 if u8 else lib.fac_forward_nchw_f32
+        _lib.check(fn(self._ctx, x.data_ptr(), B, pidx.data_ptr(), logits.data_ptr(),
+                      probs.data_ptr() if probs is not None else None, stream), self._ctx, fn.__name__)
+        return logits, probs
+
+    def forward(self, img: torch.Tensor, mask=None, pos_index=None) -> torch.Tensor:
+        if mask is not None:
+            raise NotImplementedError("mask is not supported by the HIP path (cvit_prediction.py never passes one)")
+        if img.dim() != 4 or tuple(img.shape[1:]) != (3, 224, 224):
+            raise ValueError(f"expected img [B,3,224,224], got {tuple(img.shape)}")
+        x = img.to(torch.float32).contiguous()
+        logits, _ = self._run(x, x.shape[0], pos_index, u8=False, want_probs=False)
+        return logits
+
+    def forward_u8(self, crops: torch.Tensor, pos_index=None, return_probs: bool = False):
+        """uint8 NHWC RGB face crops [B,224,224,3] -> logits (and per-logit sigmoids)."""
+        if crops.dtype != torch.uint8 or crops.dim() != 4 or tuple(crops.shape[1:]) != (224, 224, 3):
+            raise ValueError(f"expected uint8 crops [B,224,224,3], got {crops.dtype} {tuple(crops.shape)}")
+        x = crops.contiguous()
+        logits, probs = self._run(x, x.shape[0], pos_index, u8=True, want_probs=return_probs)
+        return (logits, probs) if return_probs else logits

@@ -1,0 +1,120 @@
+/*
+ * fac_cvit.h - C ABI of the MI355X (gfx950) CViT per-crop face-forgery path.
+ *
+ * Drop-in boundary for the reference's hot path.  The reference has no FFI:
+ * its boundary is the Python class `CViT` (CViT-main/model/cvit.py:80-179)
+ * that `cvit_prediction.py:20,24,62-70` imports, loads a state_dict into and
+ * calls under torch.no_grad().  Each entry point below replaces one piece of
+ * that contract; the Python mirror (fac_fake_amd/cvit.py) binds them with
+ * ctypes and keeps the reference's class name, constructor, state_dict keys
+ * and forward() semantics.  See INTEGRATION.md for the bindings.
+ *
+ * Conventions: plain pointers and sizes only.  Pointers named d_* are device
+ * pointers owned by the caller; `stream` is a hipStream_t (NULL = default
+ * stream).  Every call returns 0 (FAC_OK) or a negative fac_status and never
+ * throws; fac_last_error() describes the last failure on a context.  All work
+ * is stream-ordered with no host synchronisation, so a forward call can be
+ * captured into a hipGraph once fac_reserve() has sized the workspace.
+ */
+#ifndef FAC_CVIT_H
+#define FAC_CVIT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fac_ctx fac_ctx;
+
+typedef enum {
+  FAC_OK = 0,
+  FAC_ERR_ARG = -1,        /* null pointer / bad enum / bad size */
+  FAC_ERR_SHAPE = -2,      /* tensor shape does not match the CViT config */
+  FAC_ERR_MISSING = -3,    /* a required state_dict key was not supplied */
+  FAC_ERR_HIP = -4,        /* HIP runtime error (message in fac_last_error) */
+  FAC_ERR_NOT_LOADED = -5, /* forward before fac_load_weights */
+  FAC_ERR_OOM = -6         /* device allocation failed */
+} fac_status;
+
+/* Operand type of the MFMA path (accumulation and epilogues are fp32). */
+typedef enum { FAC_DTYPE_BF16 = 0, FAC_DTYPE_F16 = 1 } fac_dtype;
+
+/* One host fp32 tensor of a CViT state_dict (cvit_train.py:210 layout).
+ * `name` is the state_dict key, e.g. "features.0.weight". */
+typedef struct {
+  const char* name;
+  const float* data;
+  int ndim;
+  int64_t shape[4];
+} fac_tensor_desc;
+
+/* Replaces `CViT(image_size=224, patch_size=7, num_classes=2, channels=512,
+ * dim=1024, depth=6, heads=8, mlp_dim=2048).to(device)`
+ * (cvit.py:81-82, cvit_prediction.py:62-64).  Only that configuration is
+ * supported. */
+int fac_create(int device, int dtype, fac_ctx** out);
+
+/* Replaces `model.load_state_dict(sd)` (cvit_prediction.py:67-69).  Takes the
+ * 193-key state_dict as host fp32 tensors (num_batches_tracked keys may be
+ * omitted), folds eval-mode BatchNorm into the convs, repacks to NHWC/K-major
+ * 16-bit and uploads.  Synchronous. */
+int fac_load_weights(fac_ctx* ctx, const fac_tensor_desc* descs, int n);
+
+/* Size the device workspace for batches of up to max_batch crops (allocates;
+ * call before graph capture).  forward() grows it on demand otherwise. */
+int fac_reserve(fac_ctx* ctx, int max_batch);
+
+/* Bytes of device workspace a batch of B crops needs. */
+int fac_workspace_bytes(fac_ctx* ctx, int B, size_t* out);
+
+/* Replaces `model(x)` (cvit.py:167-179 via cvit_prediction.py:229):
+ * d_in = normalised fp32 NCHW [B,3,224,224]; d_pos_index = int32 [B] batch
+ * slot of each crop in [0,32) (pos_embedding row, cvit.py:154,175);
+ * d_logits = fp32 [B,2]; d_probs = fp32 [B,2] per-logit sigmoid (pred_sig,
+ * cvit_prediction.py:258-259) or NULL. */
+int fac_forward_nchw_f32(fac_ctx* ctx, const float* d_in, int B, const int32_t* d_pos_index, float* d_logits,
+                         float* d_probs, void* stream);
+
+/* Same, from raw uint8 NHWC face crops [B,224,224,3] (RGB, the crop format of
+ * cvit_prediction.py:106-121,202): the /255 + ImageNet normalisation of
+ * cvit_prediction.py:41-45,212-215 is fused into conv1. */
+int fac_forward_nhwc_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
+                        float* d_probs, void* stream);
+
+/* Test/measurement entry points ------------------------------------------
+ * fac_debug_features_u8: run conv1..conv{layer+1} (layer 0..16) on uint8
+ * crops and copy that block's NHWC 16-bit output (after ReLU, and after the
+ * MaxPool where one follows) to d_out.  For per-layer parity tests.
+ * fac_profile_forward_u8: one forward with a hipEvent between stages;
+ * synchronises and writes FAC_PROFILE_STAGES durations (ms): conv1..conv17,
+ * patch embedding, transformer (6 layers), head. */
+#define FAC_PROFILE_STAGES 20
+int fac_debug_features_u8(fac_ctx* ctx, const uint8_t* d_in, int B, int layer, uint16_t* d_out, void* stream);
+int fac_profile_forward_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
+                           float* stage_ms, int n_stages, void* stream);
+
+/* Nonzero if a previous forward saw a pos_index outside [0,32) (clamped).
+ * Synchronises the context's device; not for use inside graph capture. */
+int fac_check_device_errors(fac_ctx* ctx, int* flags);
+
+/* Video-level score over n logit pairs (pred_sig + pre_process_prediction,
+ * cvit_prediction.py:240,258-281): d_score = fp32 scalar. */
+int fac_video_score(const float* d_logits, int n, float* d_score, void* stream);
+
+/* Tuning knob: run the conv stem in sub-batches of `crops` crops (0 = whole
+ * batch), so intermediate activations stay resident in the Infinity Cache. */
+int fac_set_stem_chunk(fac_ctx* ctx, int crops);
+
+const char* fac_last_error(fac_ctx* ctx);
+void fac_destroy(fac_ctx* ctx);
+
+/* Library version / build string (for logs). */
+const char* fac_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FAC_CVIT_H */

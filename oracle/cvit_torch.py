@@ -1,0 +1,157 @@
+"""ORACLE (test infrastructure, never shipped or measured as the product).
+
+CPU restatement of the reference CViT forward, ``CViT-main/model/cvit.py``,
+written functionally over a state_dict with the same PyTorch CPU ops the
+reference module calls, so it executes the same kernels:
+
+* ``forward_fp32``   - the reference arithmetic (cvit.py:167-179), fp32.
+                        Pinned against goldens produced by the reference
+                        itself (tests/golden/, tools/make_golden.py).  Also
+                        the ``cpu_baseline`` leg of bench.py (kind "port").
+* ``forward_emulated``- the same network with operands rounded to bf16/fp16
+                        exactly where the gfx950 path rounds them (BN folded
+                        then rounded weights, 16-bit activations between
+                        layers, fp32 accumulation and epilogues).  Used to
+                        check the HIP kernels tightly; the fp32 goldens check
+                        end-to-end parity.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may import
+this package.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+MEAN = (0.485, 0.456, 0.406)     # cvit_prediction.py:41
+STD = (0.229, 0.224, 0.225)      # cvit_prediction.py:42
+BN_EPS = 1e-5                    # nn.BatchNorm2d default (cvit.py:89..146)
+LN_EPS = 1e-5                    # nn.LayerNorm default (cvit.py:16)
+STEM = [(3, 32), (32, 32), (32, 32), (32, 64), (64, 64), (64, 64), (64, 128), (128, 128), (128, 128),
+        (128, 256), (256, 256), (256, 256), (256, 256), (256, 512), (512, 512), (512, 512), (512, 512)]
+POOL_AFTER = {2, 5, 8, 12, 16}   # MaxPool2d(2,2) at cvit.py:97,108,119,133,147
+
+
+def stem_indices():
+    """(conv, bn) nn.Sequential indices of the 17 convs (cvit.py:86-148)."""
+    out, idx = [], 0
+    for i in range(17):
+        out.append((idx, idx + 1))
+        idx += 3 + (1 if i in POOL_AFTER else 0)
+    return out
+
+
+def to_torch_sd(sd) -> dict:
+    return {k: torch.as_tensor(v) for k, v in sd.items()}
+
+
+def normalize_u8(crops_u8) -> torch.Tensor:
+    """uint8 NHWC -> normalised fp32 NCHW, in the reference's op order
+    (cvit_prediction.py:209-215: .float(), permute, /255., Normalize)."""
+    x = torch.as_tensor(crops_u8).float().permute(0, 3, 1, 2)
+    x = x / 255.
+    mean = torch.tensor(MEAN, dtype=torch.float32).view(1, 3, 1, 1)
+    std = torch.tensor(STD, dtype=torch.float32).view(1, 3, 1, 1)
+    return ((x - mean) / std).contiguous()
+
+
+def _pos_rows(sd, pos_index, B):
+    pos = sd["pos_embedding"]  # [32,1,dim]
+    if pos_index is None:
+        return pos[0:B]        # cvit.py:175 (raises past 32 crops, like the reference)
+    return pos[torch.as_tensor(pos_index, dtype=torch.long)]
+
+
+def _transformer(sd, x, depth=6, heads=8, lin=None, act_round=None):
+    """6 x {x += to_out(attn(LN(x))); x += FF(LN(x))} (cvit.py:5-78)."""
+    lin = lin or (lambda inp, w, b=None: F.linear(inp, w, b))
+    rnd = act_round or (lambda t: t)
+    B, n, dim = x.shape
+    scale = dim ** -0.5        # cvit.py:38 uses dim, not the head width
+    for l in range(depth):
+        p = f"transformer.layers.{l}."
+        h = F.layer_norm(x, (dim,), sd[p + "0.fn.norm.weight"], sd[p + "0.fn.norm.bias"], LN_EPS)
+        qkv = lin(rnd(h), sd[p + "0.fn.fn.to_qkv.weight"])
+        q, k, v = qkv.view(B, n, 3, heads, dim // heads).permute(2, 0, 3, 1, 4)
+        att = (torch.einsum("bhid,bhjd->bhij", q, k) * scale).softmax(dim=-1)
+        o = torch.einsum("bhij,bhjd->bhid", att, v).permute(0, 2, 1, 3).reshape(B, n, dim)
+        x = lin(rnd(o), sd[p + "0.fn.fn.to_out.weight"], sd[p + "0.fn.fn.to_out.bias"]) + x
+        h = F.layer_norm(x, (dim,), sd[p + "1.fn.norm.weight"], sd[p + "1.fn.norm.bias"], LN_EPS)
+        h = F.gelu(lin(rnd(h), sd[p + "1.fn.fn.net.0.weight"], sd[p + "1.fn.fn.net.0.bias"]))
+        x = lin(rnd(h), sd[p + "1.fn.fn.net.2.weight"], sd[p + "1.fn.fn.net.2.bias"]) + x
+    return x
+
+
+@torch.no_grad()
+def forward_fp32(sd, img: torch.Tensor, pos_index=None, return_features: bool = False):
+    """Reference CViT.forward (cvit.py:167-179) on normalised fp32 NCHW input."""
+    sd = to_torch_sd(sd)
+    h = img.float()
+    feats = []
+    for i, (ci, bi) in enumerate(stem_indices()):
+        p, q = f"features.{ci}.", f"features.{bi}."
+        h = F.conv2d(h, sd[p + "weight"], sd[p + "bias"], padding=1)
+        h = F.batch_norm(h, sd[q + "running_mean"], sd[q + "running_var"], sd[q + "weight"], sd[q + "bias"],
+                         False, 0.1, BN_EPS)
+        h = F.relu(h)
+        if i in POOL_AFTER:
+            h = F.max_pool2d(h, 2, 2)
+        feats.append(h)
+    B = h.shape[0]
+    y = h.permute(0, 2, 3, 1).reshape(B, 1, -1)  # 'b c (h p1) (w p2) -> b (h w) (p1 p2 c)' with h=w=1
+    y = F.linear(y, sd["patch_to_embedding.weight"], sd["patch_to_embedding.bias"])
+    x = torch.cat((sd["cls_token"].expand(B, -1, -1), y), 1)
+    x = x + _pos_rows(sd, pos_index, B)
+    x = _transformer(sd, x)
+    c = x[:, 0]
+    out = F.linear(F.relu(F.linear(c, sd["mlp_head.0.weight"], sd["mlp_head.0.bias"])), sd["mlp_head.2.weight"],
+                   sd["mlp_head.2.bias"])
+    return (out, feats) if return_features else out
+
+
+def round_to(t: torch.Tensor, dtype: str) -> torch.Tensor:
+    td = {"bf16": torch.bfloat16, "fp16": torch.float16}[dtype]
+    return t.to(td).float()
+
+
+def fold_bn(sd, ci, bi):
+    """BN folded into conv (fp32, same formula and op order as cvit_abi.hip)."""
+    p, q = f"features.{ci}.", f"features.{bi}."
+    s = sd[q + "weight"] / torch.sqrt(sd[q + "running_var"] + torch.tensor(BN_EPS, dtype=torch.float32))
+    w = sd[p + "weight"] * s.view(-1, 1, 1, 1)
+    b = (sd[p + "bias"] - sd[q + "running_mean"]) * s + sd[q + "bias"]
+    return w, b
+
+
+@torch.no_grad()
+def forward_emulated(sd, img: torch.Tensor, pos_index=None, dtype: str = "bf16", return_features: bool = False):
+    """The gfx950 path's arithmetic on the CPU: 16-bit operands, fp32 accumulate.
+
+    Rounding points (cf. conv.hip / transformer.hip): the normalised input;
+    every folded conv weight; every conv output after bias+ReLU(+pool); the
+    patch-embed and transformer/head weight matrices; LayerNorm outputs; the
+    attention output; the GELU output; the CLS rows entering the head.  fp32:
+    conv/BN biases, the residual stream, QKV, softmax, LN statistics, the
+    final 2048->2 layer and its input.
+    """
+    sd = to_torch_sd(sd)
+    r = lambda t: round_to(t, dtype)  # noqa: E731
+    h = r(img.float())
+    feats = []
+    for i, (ci, bi) in enumerate(stem_indices()):
+        w, b = fold_bn(sd, ci, bi)
+        h = F.relu(F.conv2d(h, r(w), b, padding=1))
+        if i in POOL_AFTER:
+            h = F.max_pool2d(h, 2, 2)
+        h = r(h)
+        feats.append(h)
+    B = h.shape[0]
+    y = h.permute(0, 2, 3, 1).reshape(B, 1, -1)
+    y = F.linear(y, r(sd["patch_to_embedding.weight"]), sd["patch_to_embedding.bias"])
+    x = torch.cat((sd["cls_token"].expand(B, -1, -1), y), 1) + _pos_rows(sd, pos_index, B)
+    lin = lambda inp, w, b=None: F.linear(inp, r(w), b)  # noqa: E731
+    x = _transformer(sd, x, lin=lin, act_round=r)
+    c = r(x[:, 0])
+    hh = F.relu(F.linear(c, r(sd["mlp_head.0.weight"]), sd["mlp_head.0.bias"]))
+    out = F.linear(hh, sd["mlp_head.2.weight"], sd["mlp_head.2.bias"])
+    return (out, feats) if return_features else out

@@ -1,0 +1,127 @@
+"""Host-side checks that need no GPU: the C ABI library and the Python mirror."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+REPO = Path(__file__).resolve().parents[1]
+
+
+def _header_symbols():
+    text = (REPO / "include" / "fac_cvit.h").read_text()
+    return sorted(set(re.findall(r"\b(fac_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_abi():
+    syms = _header_symbols()
+    for s in ("fac_create", "fac_load_weights", "fac_forward_nchw_f32", "fac_forward_nhwc_u8", "fac_destroy",
+              "fac_last_error", "fac_reserve", "fac_video_score"):
+        assert s in syms
+
+
+def test_library_loads_and_exports_every_symbol(built_lib):
+    lib = ctypes.CDLL(str(built_lib))
+    for s in _header_symbols():
+        assert hasattr(lib, s), s
+    from fac_fake_amd import _lib
+    assert set(_header_symbols()) == set(_lib.SIGNATURES)
+
+
+def test_library_is_gfx950_code(built_lib):
+    data = built_lib.read_bytes()
+    assert b"gfx950" in data
+    assert b"__hip_fatbin" in data or b"HIPF" in data or b"__CLANG_OFFLOAD_BUNDLE__" in data
+
+
+def test_version_and_null_safety(built_lib):
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    assert lib.fac_version().decode().startswith("fac_cvit")
+    assert lib.fac_create(0, 7, None) == -1                       # bad dtype / null out
+    assert lib.fac_load_weights(None, None, 0) == -1
+    assert lib.fac_forward_nhwc_u8(None, None, 1, None, None, None, None) == -1
+    assert lib.fac_last_error(None) == b"null context"
+    lib.fac_destroy(None)
+
+
+def test_state_dict_is_the_reference_layout(golden):
+    from fac_fake_amd.cvit import CViT
+    want = list(golden("weights_checksums.json"))
+    m = CViT()
+    sd = m.state_dict()
+    assert list(sd) == want
+    assert sd["features.1.num_batches_tracked"].dtype == torch.long
+    assert tuple(sd["patch_to_embedding.weight"].shape) == (1024, 25088)
+    assert tuple(sd["pos_embedding"].shape) == (32, 1, 1024)
+
+
+def test_load_state_dict_roundtrip(sd):
+    from fac_fake_amd.cvit import CViT
+    m = CViT(dtype="fp16")
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    got = m.state_dict()
+    assert all(np.array_equal(got[k].numpy(), np.asarray(sd[k])) for k in sd)
+    with pytest.raises(RuntimeError):
+        m.load_state_dict({"pos_embedding": torch.zeros(32, 1, 1024)})   # strict, like nn.Module
+
+
+def test_constructor_contract():
+    from fac_fake_amd.cvit import CViT
+    with pytest.raises(AssertionError):
+        CViT(image_size=225)
+    with pytest.raises(NotImplementedError):
+        CViT(depth=4)
+    with pytest.raises(ValueError):
+        CViT(dtype="fp8")
+    m = CViT()
+    assert not m.training
+    with pytest.raises(RuntimeError):
+        m.train()
+
+
+def test_forward_fails_loudly_without_gpu():
+    from fac_fake_amd.cvit import CViT
+    m = CViT()
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 224, 224))
+    with pytest.raises(NotImplementedError):
+        m(torch.zeros(1, 3, 224, 224), mask=torch.ones(1, 1, dtype=torch.bool))
+    with pytest.raises(ValueError):
+        m(torch.zeros(1, 3, 112, 112))
+
+
+def test_pos_index_rules():
+    from fac_fake_amd.cvit import CViT
+    p = CViT._pos_index(5, None, "cpu")
+    assert p.tolist() == [0, 1, 2, 3, 4] and p.dtype == torch.int32
+    with pytest.raises(RuntimeError, match="must match"):
+        CViT._pos_index(33, None, "cpu")
+    with pytest.raises(IndexError):
+        CViT._pos_index(2, [0, 32], "cpu")
+    with pytest.raises(ValueError):
+        CViT._pos_index(2, [0], "cpu")
+    assert CViT._pos_index(40, np.arange(40) % 32, "cpu").tolist()[32:] == list(range(8))
+
+
+def test_drop_in_import_path():
+    """`sys.path.insert(1, 'model'); from cvit import CViT` resolves to the HIP module."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("cvit_dropin", REPO / "model" / "cvit.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    from fac_fake_amd.cvit import CViT
+    assert mod.CViT is CViT
+
+
+def test_sharding_bounds():
+    from fac_fake_amd.sharding import shard_bounds
+    for n in (0, 1, 7, 29, 300, 301):
+        for w in (1, 2, 3, 8):
+            spans = [shard_bounds(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1
