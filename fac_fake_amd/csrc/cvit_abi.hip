@@ -118,7 +118,10 @@ int set_err(fac_ctx* c, int code, const std::string& msg) {
 
 uint16_t to16(int dtype, float f) { return dtype == 0 ? fac_host::f32_to_bf16(f) : fac_host::f32_to_f16(f); }
 
-int patch_splits(int B) { return B <= 64 ? 28 : 8; }
+// Split-K factor of the patch embedding (K = 25088 = 392 k-tiles of 64).  Fixed,
+// so a crop's logits are bit-identical whatever batch it is scored in.
+constexpr int kPatchSplits = 14;
+int patch_splits(int) { return kPatchSplits; }
 
 struct WsLayout {
   size_t act, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, total;
@@ -128,7 +131,7 @@ WsLayout layout(int B, int chunk) {
   auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
   WsLayout L{};
   const int cb = (chunk > 0 && chunk < B) ? chunk : B;
-  const size_t S = (size_t)std::max(patch_splits(B) * std::min(B, 64), 8 * B);
+  const size_t S = (size_t)kPatchSplits * B;
   size_t off = 0;
   L.act = off; off += 2 * al((size_t)cb * kImg * kImg * 32 * 2);
   L.stem = off; off += al((size_t)B * kPatchDim * 2);
@@ -343,11 +346,13 @@ struct Prof {
 };
 
 int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
-                 void* stream, Prof* prof = nullptr, int stop_after = -1, uint16_t* feat_out = nullptr) {
+                 void* stream, Prof* prof = nullptr, int stop_after = -1, uint16_t* feat_out = nullptr,
+                 const uint16_t* stem_in = nullptr) {
   using namespace fac;
   if (!c) return FAC_ERR_ARG;
   if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "forward before fac_load_weights");
-  if (B <= 0 || !in || (stop_after < 0 && (!pidx || !logits))) return set_err(c, FAC_ERR_ARG, "bad forward arguments");
+  if (B <= 0 || (!in && !stem_in) || (stop_after < 0 && (!pidx || !logits)))
+    return set_err(c, FAC_ERR_ARG, "bad forward arguments");
   DevGuard g(c->device);
   int rc = ensure_ws(c, B);
   if (rc) return rc;
@@ -359,7 +364,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     if (prof) HIP_TRY(c, hipEventRecord(prof->ev[prof->n++], st));  \
   } while (0)
   MARK();
-  for (int b0 = 0; b0 < B; b0 += chunk) {
+  for (int b0 = 0; b0 < B && !stem_in; b0 += chunk) {
     const int nb = std::min(chunk, B - b0);
     const void* src = u8 ? (const void*)((const uint8_t*)in + (size_t)b0 * kImg * kImg * 3)
                          : (const void*)((const float*)in + (size_t)b0 * 3 * kImg * kImg);
@@ -384,7 +389,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     }
   }
   const int S = patch_splits(B);
-  HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->stem_out, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
+  HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, stem_in ? stem_in : c->stem_out, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
                          kPatchDim, S, st));
   HIP_TRY(c, launch_embed_finalize(c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->errflag, st));
   MARK();
@@ -472,6 +477,20 @@ int fac_forward_nhwc_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d
 int fac_debug_features_u8(fac_ctx* c, const uint8_t* d_in, int B, int layer, uint16_t* d_out, void* stream) {
   if (!c || !d_out || layer < 0 || layer > 16) return set_err(c, FAC_ERR_ARG, "bad debug_features arguments");
   return forward_impl(c, d_in, true, B, nullptr, nullptr, nullptr, stream, nullptr, layer, d_out);
+}
+
+int fac_debug_conv(fac_ctx* c, int layer, const uint16_t* d_in, int B, uint16_t* d_out, void* stream) {
+  if (!c || !d_in || !d_out || B <= 0 || layer < 1 || layer > 16) return set_err(c, FAC_ERR_ARG, "bad debug_conv arguments");
+  if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "debug_conv before fac_load_weights");
+  DevGuard g(c->device);
+  const ConvLayer& L = c->conv[layer - 1];
+  HIP_TRY(c, fac::launch_conv3x3(c->dtype, d_in, L.w, L.b, d_out, B, L.H, L.H, L.Cin, L.Cout, L.pool, (hipStream_t)stream));
+  return FAC_OK;
+}
+
+int fac_debug_tail(fac_ctx* c, const uint16_t* d_stem, int B, const int32_t* d_pos, float* d_logits, void* stream) {
+  if (!d_stem) return set_err(c, FAC_ERR_ARG, "bad debug_tail arguments");
+  return forward_impl(c, nullptr, true, B, d_pos, d_logits, nullptr, stream, nullptr, -1, nullptr, d_stem);
 }
 
 int fac_profile_forward_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits,

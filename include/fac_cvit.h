@@ -89,9 +89,15 @@ int fac_forward_nhwc_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t*
  * MaxPool where one follows) to d_out.  For per-layer parity tests.
  * fac_profile_forward_u8: one forward with a hipEvent between stages;
  * synchronises and writes FAC_PROFILE_STAGES durations (ms): conv1..conv17,
- * patch embedding, transformer (6 layers), head. */
+ * patch embedding, transformer (6 layers), head.
+ * fac_debug_conv: run stem conv `layer` (1..16 = conv2..conv17) alone on a
+ * given NHWC 16-bit input.  fac_debug_tail: patch embedding + transformer +
+ * head from a given NHWC 16-bit stem output [B,7,7,512]. */
 #define FAC_PROFILE_STAGES 20
 int fac_debug_features_u8(fac_ctx* ctx, const uint8_t* d_in, int B, int layer, uint16_t* d_out, void* stream);
+int fac_debug_conv(fac_ctx* ctx, int layer, const uint16_t* d_in, int B, uint16_t* d_out, void* stream);
+int fac_debug_tail(fac_ctx* ctx, const uint16_t* d_stem, int B, const int32_t* d_pos_index, float* d_logits,
+                   void* stream);
 int fac_profile_forward_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
                            float* stage_ms, int n_stages, void* stream);
 

@@ -97,6 +97,14 @@ def forward_fp32(sd, img: torch.Tensor, pos_index=None, return_features: bool = 
         if i in POOL_AFTER:
             h = F.max_pool2d(h, 2, 2)
         feats.append(h)
+    out = tail_fp32(sd, h, pos_index)
+    return (out, feats) if return_features else out
+
+
+@torch.no_grad()
+def tail_fp32(sd, h: torch.Tensor, pos_index=None):
+    """Stem output [B,512,7,7] -> logits: cvit.py:170-179 in fp32."""
+    sd = to_torch_sd(sd)
     B = h.shape[0]
     y = h.permute(0, 2, 3, 1).reshape(B, 1, -1)  # 'b c (h p1) (w p2) -> b (h w) (p1 p2 c)' with h=w=1
     y = F.linear(y, sd["patch_to_embedding.weight"], sd["patch_to_embedding.bias"])
@@ -104,9 +112,8 @@ def forward_fp32(sd, img: torch.Tensor, pos_index=None, return_features: bool = 
     x = x + _pos_rows(sd, pos_index, B)
     x = _transformer(sd, x)
     c = x[:, 0]
-    out = F.linear(F.relu(F.linear(c, sd["mlp_head.0.weight"], sd["mlp_head.0.bias"])), sd["mlp_head.2.weight"],
-                   sd["mlp_head.2.bias"])
-    return (out, feats) if return_features else out
+    return F.linear(F.relu(F.linear(c, sd["mlp_head.0.weight"], sd["mlp_head.0.bias"])), sd["mlp_head.2.weight"],
+                    sd["mlp_head.2.bias"])
 
 
 def round_to(t: torch.Tensor, dtype: str) -> torch.Tensor:
@@ -145,6 +152,27 @@ def forward_emulated(sd, img: torch.Tensor, pos_index=None, dtype: str = "bf16",
             h = F.max_pool2d(h, 2, 2)
         h = r(h)
         feats.append(h)
+    out = tail_emulated(sd, h, pos_index, dtype)
+    return (out, feats) if return_features else out
+
+
+@torch.no_grad()
+def conv_block_emulated(sd, h: torch.Tensor, i: int, dtype: str = "bf16") -> torch.Tensor:
+    """Conv i (0-based) alone on a 16-bit-valued NCHW input, HIP rounding points."""
+    sd = to_torch_sd(sd)
+    ci, bi = stem_indices()[i]
+    w, b = fold_bn(sd, ci, bi)
+    h = F.relu(F.conv2d(h, round_to(w, dtype), b, padding=1))
+    if i in POOL_AFTER:
+        h = F.max_pool2d(h, 2, 2)
+    return round_to(h, dtype)
+
+
+@torch.no_grad()
+def tail_emulated(sd, h: torch.Tensor, pos_index=None, dtype: str = "bf16"):
+    """Stem output (16-bit valued) -> logits with the HIP path's rounding points."""
+    sd = to_torch_sd(sd)
+    r = lambda t: round_to(t, dtype)  # noqa: E731
     B = h.shape[0]
     y = h.permute(0, 2, 3, 1).reshape(B, 1, -1)
     y = F.linear(y, r(sd["patch_to_embedding.weight"]), sd["patch_to_embedding.bias"])
@@ -153,5 +181,4 @@ def forward_emulated(sd, img: torch.Tensor, pos_index=None, dtype: str = "bf16",
     x = _transformer(sd, x, lin=lin, act_round=r)
     c = r(x[:, 0])
     hh = F.relu(F.linear(c, r(sd["mlp_head.0.weight"]), sd["mlp_head.0.bias"]))
-    out = F.linear(hh, sd["mlp_head.2.weight"], sd["mlp_head.2.bias"])
-    return (out, feats) if return_features else out
+    return F.linear(hh, sd["mlp_head.2.weight"], sd["mlp_head.2.bias"])

@@ -3,11 +3,14 @@
 Tolerances (stated per test):
 * fp16 operands: per-frame probabilities within 1e-3 of the fp32 reference
   (the north-star bar), checked against goldens the reference produced.
-* bf16 operands: exact bf16 rounding of operands already moves the fp32
-  reference by up to ~4e-3 on these weights (oracle emulation, see DESIGN.md
-  "bf16 vs the 1e-3 bar"), so bf16 is gated tightly against the oracle's
-  emulation of the same rounding points (probs within 1e-3, logits 4e-3) and
-  loosely (probs within 1e-2) against the fp32 goldens.
+* bf16 operands: exact bf16 rounding of the operands alone already moves the
+  fp32 reference by up to ~4e-3 in probability on these weights (oracle
+  emulation; DESIGN.md "bf16 vs the 1e-3 bar"), so end-to-end bf16 is gated
+  at 1e-2 against the fp32 goldens, and the kernels themselves are gated
+  tightly per kernel: each conv fed the oracle's previous-layer output agrees
+  to <= 2 ulp (1-ulp accumulation-order flips on a few % of outputs), the
+  tail fed the oracle's stem output agrees within 1e-3 in probability, and
+  the whole forward stays inside the oracle's 16-bit rounding envelope.
 """
 import numpy as np
 import pytest
@@ -91,40 +94,105 @@ def test_real_crops(models, golden, dt):
     assert dp <= (1e-3 if dt == "fp16" else 1e-2), (dt, dp)
 
 
-@pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_against_emulated_oracle(models, sd, dt, torch_threads):
-    """Tight check of the kernels: same rounding points as the oracle emulation."""
-    from oracle.cvit_torch import forward_emulated, normalize_u8
-    crops = make_crops(8, seed=11)
-    slots = np.array([0, 5, 31, 7, 7, 12, 30, 1])
-    ref = forward_emulated(sd, normalize_u8(crops), pos_index=slots, dtype=dt).numpy()
-    lg = _run_u8(models[dt], crops, slots)
-    assert np.abs(lg - ref).max() <= (1e-3 if dt == "fp16" else 4e-3), np.abs(lg - ref).max()
-    assert np.abs(_sig(lg) - _sig(ref)).max() <= 1e-3
+ULP_REL = {"fp16": 2.0 ** -10, "bf16": 2.0 ** -7}  # one unit in the last place, relative
+
+
+def _ulp_diff(got, ref, dt):
+    """|got - ref| in 16-bit ulps of max(|ref|, rms(ref)/2).
+
+    The floor matters for outputs near zero: there the fp32 accumulation-order
+    noise (relative to the summed magnitudes, not to the tiny result) exceeds
+    a 16-bit ulp of the result.  A wrong tap/channel/pixel is off by O(rms):
+    hundreds of these units."""
+    floor = 0.5 * float(ref.pow(2).mean().sqrt())
+    return ((got - ref).abs() / (ref.abs().clamp_min(floor) * ULP_REL[dt])).max().item()
+
+
+def _rms_rel(a, b):
+    return float((a - b).pow(2).mean().sqrt() / (b.pow(2).mean().sqrt() + 1e-30))
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_per_layer_features(models, sd, dt, torch_threads):
-    """Each conv block's NHWC output vs the oracle emulation (same input per layer)."""
+def test_conv1_fused_normalize_vs_oracle(models, sd, dt, torch_threads):
+    """conv1 with the uint8 -> /255 -> Normalize step fused: bit-exact but for
+    accumulation-order rounding flips (at most 1 ulp, on a tiny fraction)."""
     from fac_fake_amd import _lib
     from oracle.cvit_torch import forward_emulated, normalize_u8
     crops = make_crops(2, seed=12)
     _, feats = forward_emulated(sd, normalize_u8(crops), dtype=dt, return_features=True)
-    m = models[dt]
+    ref = feats[0].permute(0, 2, 3, 1).contiguous()
     lib = _lib.load()
     x = torch.from_numpy(crops).to(DEV)
+    out = torch.empty(ref.shape, dtype=torch.float16 if dt == "fp16" else torch.bfloat16, device=DEV)
+    _lib.check(lib.fac_debug_features_u8(models[dt]._ctx, x.data_ptr(), 2, 0, out.data_ptr(), None), None, "dbg")
+    torch.cuda.synchronize()
+    got = out.float().cpu()
+    assert float((got != ref).float().mean()) <= 1e-3
+    assert _ulp_diff(got, ref, dt) <= 1.01
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_each_conv_kernel_isolated(models, sd, dt, torch_threads):
+    """Every stem conv (conv2..conv17, all six kernel instantiations) fed the
+    oracle's previous-layer output: BN-fold, ReLU, fused max-pool and the
+    16-bit store must agree with the oracle up to 1-ulp accumulation-order
+    flips on a small fraction of outputs."""
+    from fac_fake_amd import _lib
+    from oracle.cvit_torch import conv_block_emulated, forward_emulated, normalize_u8
+    crops = make_crops(2, seed=12)
+    _, feats = forward_emulated(sd, normalize_u8(crops), dtype=dt, return_features=True)
+    lib = _lib.load()
     tdt = torch.float16 if dt == "fp16" else torch.bfloat16
-    for layer, ref in enumerate(feats):
-        ref_nhwc = ref.permute(0, 2, 3, 1).contiguous()
-        out = torch.empty(ref_nhwc.shape, dtype=tdt, device=DEV)
-        _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), 2, layer, out.data_ptr(),
-                                             torch.cuda.current_stream().cuda_stream), m._ctx, "debug_features")
+    for layer in range(1, 17):
+        inp = feats[layer - 1]
+        ref = conv_block_emulated(sd, inp, layer, dt).permute(0, 2, 3, 1).contiguous()
+        x = inp.permute(0, 2, 3, 1).contiguous().to(tdt).to(DEV)
+        out = torch.empty(ref.shape, dtype=tdt, device=DEV)
+        _lib.check(lib.fac_debug_conv(models[dt]._ctx, layer, x.data_ptr(), 2, out.data_ptr(), None), None, "conv")
         torch.cuda.synchronize()
         got = out.float().cpu()
-        scale = ref_nhwc.abs().max().item() + 1e-6
-        err = (got - ref_nhwc).abs().max().item() / scale
-        # one 16-bit ulp of relative slack, plus accumulation-order noise
-        assert err <= (4e-3 if dt == "fp16" else 2e-2), (layer, err)
+        frac = float((got != ref).float().mean())
+        assert frac <= 0.05, (layer, frac)
+        assert _ulp_diff(got, ref, dt) <= 2.01, (layer, _ulp_diff(got, ref, dt))
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_tail_isolated(models, sd, dt, torch_threads):
+    """Patch embedding + 6 transformer layers + head from the oracle's stem
+    output: within the 16-bit rounding envelope of the fp32 tail."""
+    from fac_fake_amd import _lib
+    from oracle.cvit_torch import forward_emulated, normalize_u8, tail_emulated, tail_fp32
+    crops = make_crops(8, seed=11)
+    slots = np.array([0, 5, 31, 7, 7, 12, 30, 1])
+    _, feats = forward_emulated(sd, normalize_u8(crops), dtype=dt, return_features=True)
+    stem = feats[16]
+    em = tail_emulated(sd, stem, slots, dt)
+    fp = tail_fp32(sd, stem, slots)
+    lib = _lib.load()
+    x = stem.permute(0, 2, 3, 1).contiguous().to(torch.float16 if dt == "fp16" else torch.bfloat16).to(DEV)
+    p = torch.from_numpy(slots.astype(np.int32)).to(DEV)
+    out = torch.empty(8, 2, device=DEV)
+    _lib.check(lib.fac_debug_tail(models[dt]._ctx, x.data_ptr(), 8, p.data_ptr(), out.data_ptr(), None), None, "tail")
+    torch.cuda.synchronize()
+    got = out.cpu()
+    print(dt, "tail gpu-emu", float((got - em).abs().max()), "emu-fp32", float((em - fp).abs().max()),
+          "gpu-fp32", float((got - fp).abs().max()))
+    assert _rms_rel(got, fp) <= 1.5 * _rms_rel(em, fp) + 1e-4
+    assert np.abs(_sig(got.numpy()) - _sig(em.numpy())).max() <= 1e-3
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_error_envelope_end_to_end(models, sd, dt, torch_threads):
+    """Whole forward: the HIP path's distance from fp32 is what exact 16-bit
+    rounding at its rounding points gives (oracle emulation), not more."""
+    from oracle.cvit_torch import forward_emulated, forward_fp32, normalize_u8
+    crops = make_crops(8, seed=11)
+    slots = np.array([0, 5, 31, 7, 7, 12, 30, 1])
+    x = normalize_u8(crops)
+    em = forward_emulated(sd, x, pos_index=slots, dtype=dt)
+    fp = forward_fp32(sd, x, pos_index=slots)
+    got = torch.from_numpy(_run_u8(models[dt], crops, slots))
+    assert _rms_rel(got, fp) <= 1.6 * _rms_rel(em, fp) + 1e-4, (_rms_rel(got, fp), _rms_rel(em, fp))
 
 
 def test_nchw_f32_matches_u8(models):
@@ -209,11 +277,11 @@ def test_graph_capture_replay_matches_eager(models):
 
 
 def test_large_batch_properties(models):
-    """B=512 (beyond the goldens): finite, and crop j equals the B=64 result of the same crop+slot."""
+    """B=512 (beyond the goldens): finite, and bit-identical to scoring the same crops as a B=64 batch."""
     m = models["fp16"]
     crops = make_crops(512, seed=16)
     slots = np.arange(512) % 32
     big = _run_u8(m, crops, slots)
     assert np.isfinite(big).all()
     small = _run_u8(m, crops[448:], slots[448:])
-    assert np.abs(_sig(big[448:]) - _sig(small)).max() <= 1e-5
+    assert np.array_equal(big[448:], small)     # a crop's logits do not depend on its batch
