@@ -19,8 +19,18 @@
 
 namespace fac {
 
-constexpr int CONV_CK = 32;           // input channels per K chunk
-constexpr int CONV_PS = CONV_CK + 8;  // LDS row stride (elements) = 80 B
+constexpr int CONV_CK = 32;  // input channels per K chunk (= 4 x 16-byte "q" pieces)
+
+// LDS images (16-byte units), chosen by simulating the ds_read_b128 lane
+// groups of MI355X_MICROARCH.md §LDS over every tap and row tile:
+//  * halo: q-major planes [q][hy][hx], row pitch HALO_RP = 24 (== 8 mod 16,
+//    so the 2x8-pixel strip one 16-row tile covers hits 16 distinct slots)
+//    and plane pitch (TH+2)*24 + 8: A-fragment reads conflict-free for 16x16
+//    boxes (1.4-way average for 14x14), staging writes 2-way.
+//  * weight slice: q-major [q][BN], identical to its global packing
+//    [n-block][chunk][tap][q][BN][8], so staging is a linear 16-byte copy and
+//    B-fragment reads are conflict-free.
+constexpr int HALO_RP = 24;
 
 template <int TW>
 __device__ __forceinline__ void box_pixel(int m, int& py, int& px) {
@@ -55,23 +65,24 @@ __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, 
 }
 
 template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL>
-__global__ __launch_bounds__(256) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
+__global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
                                                        int Cin, int Cout) {
-  constexpr int CK = CONV_CK, PS = CONV_PS;
+  constexpr int CK = CONV_CK;
   constexpr int HH = TH + 2, HWD = TW + 2;
+  constexpr int NHP = HH * HALO_RP + 8;     // halo plane pitch (16-byte units)
   constexpr int NPIX = TH * TW;
   constexpr int RT = ((NPIX + 15) / 16 + WM - 1) / WM * WM;
   constexpr int RTW = RT / WM;
   constexpr int CTW = BN / 16 / WN;
-  constexpr int HALO = HH * HWD * PS;
-  constexpr int WSL = BN * PS;
+  constexpr int HALO = 4 * NHP * 8;         // elements per halo buffer
+  constexpr int WSL = BN * CK;              // elements per tap slice
   constexpr int OPIX = POOL ? NPIX / 4 : NPIX;
   constexpr int OPS = BN + 8;
-  constexpr int OPER = 2 * HALO + 2 * WSL;
-  constexpr int OSTG = OPIX * OPS;
+  constexpr int OPER = 2 * HALO + 3 * WSL;           // halo double buffer + 3-slot weight ring
+  constexpr int OSTG = (POOL ? RT * 4 : RT * 16) * OPS;  // padded: epilogue writes unguarded
   constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
   constexpr int HITEMS = HH * HWD * 4;
   constexpr int HLOADS = (HITEMS + 255) / 256;
@@ -91,48 +102,50 @@ __global__ __launch_bounds__(256) void conv3x3_bn_relu(const uint16_t* __restric
   const int y0 = ty * TH, x0 = tx * TW;
   const int nb = blockIdx.y;
   const int nchunks = Cin / CK;
-  const int nsteps = nchunks * 9;
   const uint16_t* in_b = in + (size_t)b * H * W * Cin;
-  const uint16_t* wblk = wpk + (size_t)nb * nchunks * 9 * BN * CK;
+  const uint16_t* wsrc = wpk + (size_t)nb * nchunks * 9 * WSL;
 
+  // Halo staging map, fixed across chunks: element offset of each of this
+  // thread's 16-byte pieces in the image (-1 = zero padding / unused) and its
+  // place in the LDS image (-1 = unused).
+  int hsrc[HLOADS], hdst[HLOADS];
+#pragma unroll
+  for (int i = 0; i < HLOADS; ++i) {
+    const int it = tid + 256 * i;
+    hsrc[i] = -1;
+    hdst[i] = -1;
+    if (it < HITEMS) {
+      const int p = it >> 2, q = it & 3;
+      const int hy = p / HWD, hx = p - (p / HWD) * HWD;
+      const int y = y0 + hy - 1, x = x0 + hx - 1;
+      if (y >= 0 && y < H && x >= 0 && x < W) hsrc[i] = (y * W + x) * Cin + q * 8;
+      hdst[i] = (q * NHP + hy * HALO_RP + hx) * 8;
+    }
+  }
   u16x8 hreg[HLOADS];
-  u16x8 wreg[WLOADS];
-
+  u16x8 wreg[3][WLOADS];  // register sets of the weight ring (set = slot = step % 3)
   auto load_halo = [&](int c) {
 #pragma unroll
-    for (int i = 0; i < HLOADS; ++i) {
-      const int it = tid + 256 * i;
-      u16x8 v = (u16x8)0;
-      if (it < HITEMS) {
-        const int p = it >> 2, q = it & 3;
-        const int hy = p / HWD, hx = p - (p / HWD) * HWD;
-        const int y = y0 + hy - 1, x = x0 + hx - 1;
-        if (y >= 0 && y < H && x >= 0 && x < W)
-          v = *(const u16x8*)(in_b + ((size_t)y * W + x) * Cin + c * CK + q * 8);
-      }
-      hreg[i] = v;
-    }
+    for (int i = 0; i < HLOADS; ++i)
+      hreg[i] = hsrc[i] >= 0 ? *(const u16x8*)(in_b + hsrc[i] + c * CK) : (u16x8)0;
   };
-  auto store_halo = [&](int buf) {
+  auto store_halo = [&](uint16_t* dst) {
 #pragma unroll
-    for (int i = 0; i < HLOADS; ++i) {
-      const int it = tid + 256 * i;
-      if (it < HITEMS) *(u16x8*)(smem + buf * HALO + (it >> 2) * PS + (it & 3) * 8) = hreg[i];
-    }
+    for (int i = 0; i < HLOADS; ++i)
+      if (hdst[i] >= 0) *(u16x8*)(dst + hdst[i]) = hreg[i];
   };
-  auto load_w = [&](int s) {
-    const uint16_t* src = wblk + (size_t)s * BN * CK;
+  auto load_w = [&](u16x8* r, const uint16_t* src) {
 #pragma unroll
     for (int i = 0; i < WLOADS; ++i) {
       const int it = tid + 256 * i;
-      if (it < WITEMS) wreg[i] = *(const u16x8*)(src + it * 8);
+      if (WITEMS % 256 == 0 || it < WITEMS) r[i] = *(const u16x8*)(src + it * 8);
     }
   };
-  auto store_w = [&](int buf) {
+  auto store_w = [&](const u16x8* r, uint16_t* dst) {
 #pragma unroll
     for (int i = 0; i < WLOADS; ++i) {
       const int it = tid + 256 * i;
-      if (it < WITEMS) *(u16x8*)(smem + 2 * HALO + buf * WSL + (it >> 2) * PS + (it & 3) * 8) = wreg[i];
+      if (WITEMS % 256 == 0 || it < WITEMS) *(u16x8*)(dst + it * 8) = r[i];
     }
   };
 
@@ -143,11 +156,11 @@ __global__ __launch_bounds__(256) void conv3x3_bn_relu(const uint16_t* __restric
     if (m >= NPIX) m = 0;  // padding rows: computed on pixel 0, never stored
     int py, px;
     box_pixel<TW>(m, py, px);
-    abase[rt] = (py * HWD + px) * PS + (lane >> 4) * 8;
+    abase[rt] = ((lane >> 4) * NHP + py * HALO_RP + px) * 8;
   }
   int bbase[CTW];
 #pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) bbase[ct] = ((wn * CTW + ct) * 16 + (lane & 15)) * PS + (lane >> 4) * 8;
+  for (int ct = 0; ct < CTW; ++ct) bbase[ct] = ((lane >> 4) * BN + (wn * CTW + ct) * 16 + (lane & 15)) * 8;
 
   f32x4 acc[RTW][CTW];
 #pragma unroll
@@ -155,33 +168,48 @@ __global__ __launch_bounds__(256) void conv3x3_bn_relu(const uint16_t* __restric
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = (f32x4)0.f;
 
+  // K loop: chunks of 32 input channels (runtime) x 9 taps (unrolled, so LDS
+  // offsets are immediates).  Weight slice s = 9c + t lives in ring slot s % 3
+  // = t % 3 (9 is a multiple of 3): it is fetched into register set s % 3 at
+  // the top of step s-2 and written to LDS at the end of step s-1, so each
+  // fetch has two steps of MFMA work to land.  The next chunk's halo is
+  // fetched at t = 0 and written at t = 8.
+  uint16_t* const wring = smem + 2 * HALO;
+  const int nsteps = nchunks * 9;
   load_halo(0);
-  load_w(0);
-  store_halo(0);
-  store_w(0);
+  load_w(wreg[0], wsrc);
+  if (nsteps > 1) load_w(wreg[1], wsrc + WSL);
+  wsrc += 2 * WSL;
+  store_halo(smem);
+  store_w(wreg[0], wring);
   __syncthreads();
 
-  for (int s = 0; s < nsteps; ++s) {
-    const int c = s / 9, t = s - (s / 9) * 9;
-    const bool next_w = s + 1 < nsteps;
+  for (int c = 0; c < nchunks; ++c) {
+    const uint16_t* hb = smem + (c & 1) * HALO;
     const bool next_h = c + 1 < nchunks;
-    if (next_w) load_w(s + 1);
-    if (t == 0 && next_h) load_halo(c + 1);
-    const int ky = t / 3, kx = t - (t / 3) * 3;
-    const uint16_t* hb = smem + (c & 1) * HALO + (ky * HWD + kx) * PS;
-    const uint16_t* wb = smem + 2 * HALO + (s & 1) * WSL;
-    u16x8 bfr[CTW];
+    const int s0 = c * 9;
 #pragma unroll
-    for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
+    for (int t = 0; t < 9; ++t) {
+      if (s0 + t + 2 < nsteps) {
+        load_w(wreg[(t + 2) % 3], wsrc);
+        wsrc += WSL;
+      }
+      if (t == 0 && next_h) load_halo(c + 1);
+      const uint16_t* wb = wring + (t % 3) * WSL;
+      const int toff = ((t / 3) * HALO_RP + (t % 3)) * 8;
+      u16x8 bfr[CTW];
 #pragma unroll
-    for (int rt = 0; rt < RTW; ++rt) {
-      const u16x8 a = *(const u16x8*)(hb + abase[rt]);
+      for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
 #pragma unroll
-      for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(a, bfr[ct], acc[rt][ct]);
+      for (int rt = 0; rt < RTW; ++rt) {
+        const u16x8 a = *(const u16x8*)(hb + abase[rt] + toff);
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(a, bfr[ct], acc[rt][ct]);
+      }
+      if (s0 + t + 1 < nsteps) store_w(wreg[(t + 1) % 3], wring + ((t + 1) % 3) * WSL);
+      if (t == 8 && next_h) store_halo(smem + ((c + 1) & 1) * HALO);
+      __syncthreads();
     }
-    if (next_w) store_w((s + 1) & 1);
-    if (t == 8 && next_h) store_halo((c + 1) & 1);
-    __syncthreads();
   }
 
   // Epilogue: folded-BN bias + ReLU (+ 2x2 max) -> 16-bit -> LDS -> global.
@@ -196,12 +224,12 @@ __global__ __launch_bounds__(256) void conv3x3_bn_relu(const uint16_t* __restric
       if constexpr (POOL) {
         const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
         const int w = (wm * RTW + rt) * 4 + (lane >> 4);
-        if (w < OPIX) ostg[w * OPS + nl] = T::from_f32(fmaxf(mx + bv, 0.f));
+        ostg[w * OPS + nl] = T::from_f32(fmaxf(mx + bv, 0.f));
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int m = (wm * RTW + rt) * 16 + (lane >> 4) * 4 + j;
-          if (m < NPIX) ostg[m * OPS + nl] = T::from_f32(fmaxf(v[j] + bv, 0.f));
+          ostg[m * OPS + nl] = T::from_f32(fmaxf(v[j] + bv, 0.f));
         }
       }
     }

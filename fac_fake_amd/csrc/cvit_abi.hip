@@ -275,11 +275,13 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
       const int BN = fac::conv_block_n(H), CK = 32, nch = ci / CK;
       std::vector<uint16_t> pk((size_t)co * ci * 9);
       size_t q = 0;
+      // [n-block][chunk][tap][q][BN][8]: one tap slice is the LDS image of conv.hip
       for (int nb = 0; nb < co / BN; ++nb)
         for (int ch = 0; ch < nch; ++ch)
           for (int t = 0; t < 9; ++t)
-            for (int nl = 0; nl < BN; ++nl)
-              for (int k = 0; k < CK; ++k) pk[q++] = to16(c->dtype, wf(nb * BN + nl, ch * CK + k, t));
+            for (int qq = 0; qq < CK / 8; ++qq)
+              for (int nl = 0; nl < BN; ++nl)
+                for (int j = 0; j < 8; ++j) pk[q++] = to16(c->dtype, wf(nb * BN + nl, ch * CK + qq * 8 + j, t));
       if ((rc = upload(c, pk, &L.w))) return rc;
       if ((rc = upload(c, bf, &L.b))) return rc;
     }
