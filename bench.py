@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--stem-chunk", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-fuse", action="store_true", help="unfused conv1..conv3 (A/B of the fused 224 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
@@ -97,6 +98,8 @@ def main():
     if args.stem_chunk:
         model.set_stem_chunk(args.stem_chunk)
     ctx = model._ctx
+    if args.no_fuse:
+        _lib.check(lib.fac_set_option(ctx, b"fuse_stem224", 0), ctx, "set_option")
 
     crops = torch.from_numpy(make_crops(B, seed=3 + rank)).to(dev)      # synthetic, resident in HBM
     pidx = (torch.arange(B, device=dev) % 32).to(torch.int32)
@@ -165,9 +168,14 @@ def main():
                                               20, stream.cuda_stream), ctx, "profile")
         acc += np.frombuffer(stage_ms, dtype=np.float32)
     acc /= reps
-    conv_ms = acc[:17]
+    conv_ms = acc[:17].copy()
+    fused224 = not args.no_fuse
     dom = int(np.argmax(conv_ms))
     dom_flops = conv_layer_flops(dom, B)
+    dom_name = f"conv3x3_bn_relu ({STAGE_NAMES[dom]})"
+    if fused224 and dom == 0:   # one launch covers conv1..conv3 (+pool); count their algorithmic FLOPs
+        dom_flops = sum(conv_layer_flops(i, B) for i in range(3))
+        dom_name = "stem224_fused (conv1-conv3 + pool)"
     achieved = dom_flops / (conv_ms[dom] * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype]
 
@@ -189,9 +197,10 @@ def main():
         "config": {"workload": "config 2: CViT forward, B=256 crops per GPU per step, pos slot j mod 32",
                    "model": "CViT(224,7,2,512,1024,6,8,2048)", "global_batch": world * B, "seq_len": 2,
                    "parallelism": f"frame-sharded x{world}" + (" + RCCL logit all-gather" if world > 1 else ""),
-                   "graph": graph is not None, "stem_chunk": args.stem_chunk},
+                   "graph": graph is not None, "stem_chunk": args.stem_chunk,
+                   "fused_stem224": not args.no_fuse},
         "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
-        "roofline": {"bound": "mfma", "kernel": f"conv3x3_bn_relu ({STAGE_NAMES[dom]})",
+        "roofline": {"bound": "mfma", "kernel": dom_name,
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,
                      "launch_ms": round(float(conv_ms[dom]), 4), "flops_per_launch": dom_flops},

@@ -43,6 +43,7 @@ SIGNATURES = {
     "fac_check_device_errors": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "fac_video_score": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_set_stem_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "fac_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     "fac_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "fac_destroy": (None, [ctypes.c_void_p]),
     "fac_version": (ctypes.c_char_p, []),

@@ -23,14 +23,16 @@ constexpr int CONV_CK = 32;  // input channels per K chunk (= 4 x 16-byte "q" pi
 
 // LDS images (16-byte units), chosen by simulating the ds_read_b128 lane
 // groups of MI355X_MICROARCH.md §LDS over every tap and row tile:
-//  * halo: q-major planes [q][hy][hx], row pitch HALO_RP = 24 (== 8 mod 16,
-//    so the 2x8-pixel strip one 16-row tile covers hits 16 distinct slots)
-//    and plane pitch (TH+2)*24 + 8: A-fragment reads conflict-free for 16x16
-//    boxes (1.4-way average for 14x14), staging writes 2-way.
+//  * halo: q-major planes [q][hy][hx], row pitch RP = 24 for boxes up to 22
+//    wide, 40 for 28-wide boxes (== 8 mod 16, so the 2x8-pixel strip one
+//    16-row tile covers hits 16 distinct slots), plane pitch (TH+2)*RP + 8:
+//    A-fragment reads conflict-free for 16x16, 1.14-way for 8x28 and 4x28,
+//    1.4-way for 14x14 boxes; staging writes 2-way.
 //  * weight slice: q-major [q][BN], identical to its global packing
 //    [n-block][chunk][tap][q][BN][8], so staging is a linear 16-byte copy and
 //    B-fragment reads are conflict-free.
-constexpr int HALO_RP = 24;
+template <int TW>
+constexpr int halo_rp() { return TW + 2 <= 24 ? 24 : 40; }
 
 template <int TW>
 __device__ __forceinline__ void box_pixel(int m, int& py, int& px) {
@@ -72,6 +74,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
                                                        int Cin, int Cout) {
   constexpr int CK = CONV_CK;
   constexpr int HH = TH + 2, HWD = TW + 2;
+  constexpr int HALO_RP = halo_rp<TW>();
   constexpr int NHP = HH * HALO_RP + 8;     // halo plane pitch (16-byte units)
   constexpr int NPIX = TH * TW;
   constexpr int RT = ((NPIX + 15) / 16 + WM - 1) / WM * WM;
@@ -347,27 +350,43 @@ __global__ __launch_bounds__(256) void conv1_bn_relu(const void* __restrict__ in
 // Host launchers (C++ linkage, used by cvit_abi.hip).
 namespace fac {
 
-// Per-resolution kernel configuration; must agree with conv_block_n() and
-// the weight packing in cvit_abi.hip.
-int conv_block_n(int H) { return H >= 112 ? (H == 224 ? 32 : 64) : 128; }
+// Per-resolution kernel configuration (box TH x TW, BN output channels per
+// workgroup, WM x WN wave grid); must agree with the weight packing in
+// cvit_abi.hip, which asks conv_block_n() for BN.
+//   112: 16x16 box, BN  64, 4x1 waves (256 rows, no padding)
+//    56:  8x28 box, BN 128, 2x2 waves (224 rows, no padding)
+//    28:  4x28 box, BN 256, 1x4 waves (112 rows, no padding)
+//    14: 14x14 box, BN 128, 1x4 waves (208 rows for 196 pixels)
+// (the 224 layers normally run inside stem224.hip; the 16x16/BN 32 kernel
+// serves the unfused debug path)
+int conv_block_n(int H) {
+  switch (H) {
+    case 224: return 32;
+    case 112: return 64;
+    case 28: return 256;
+    default: return 128;
+  }
+}
+
+template <class T, int TH, int TW, int BN, int WM, int WN>
+static void launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
+                       int Cin, int Cout, bool pool, hipStream_t st) {
+  dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
+  if (pool) conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout);
+  else conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout);
+}
 
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                                 int B, int H, int W, int Cin, int Cout, bool pool, hipStream_t st) {
-  const int bn = conv_block_n(H);
-  if (H == 224 || H == 112) {
-    dim3 grid(B * (H / 16) * (W / 16), Cout / bn);
-    if (bn == 32) {
-      if (pool) conv3x3_bn_relu<T, 16, 16, 32, 4, 1, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
-      else conv3x3_bn_relu<T, 16, 16, 32, 4, 1, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
-    } else {
-      if (pool) conv3x3_bn_relu<T, 16, 16, 64, 4, 1, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
-      else conv3x3_bn_relu<T, 16, 16, 64, 4, 1, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
-    }
-  } else {
-    dim3 grid(B * (H / 14) * (W / 14), Cout / bn);
-    if (pool) conv3x3_bn_relu<T, 14, 14, 128, 2, 2, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
-    else conv3x3_bn_relu<T, 14, 14, 128, 2, 2, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, W, Cin, Cout);
+  if (W != H) return hipErrorInvalidValue;
+  switch (H) {
+    case 224: launch_box<T, 16, 16, 32, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
+    case 112: launch_box<T, 16, 16, 64, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
+    case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
+    case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
+    case 14: launch_box<T, 14, 14, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

@@ -33,10 +33,17 @@ hipError_t launch_embed_finalize(const float* slab, int S, int B, const float* b
 hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,
                             hipStream_t st);
 hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipStream_t st);
+hipError_t launch_resid_layernorm(int dtype, float* x, const float* slab, int S, const float* bias, const float* g,
+                                 const float* b, uint16_t* y, int R, hipStream_t st);
+hipError_t launch_resid_cls(int dtype, const float* x, const float* slab, int S, const float* bias, uint16_t* c, int B,
+                            hipStream_t st);
 hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, float scale, hipStream_t st);
 hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, float* logits, float* probs, int B,
                            hipStream_t st);
 hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st);
+hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
+                          const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
+                          hipStream_t st);
 enum { EPI_F32 = 0, EPI_F32_RELU = 1, EPI_T_GELU = 2, EPI_RESID = 3, EPI_PARTIAL = 4, EPI_T = 5 };
 }  // namespace fac
 
@@ -96,6 +103,8 @@ struct fac_ctx {
   size_t ws_bytes = 0;
   int cap_B = 0;
   int stem_chunk = 0;
+  int fuse_stem224 = 1;  // conv1..conv3+pool as one persistent kernel (stem224.hip)
+  int num_cu = 256;
   uint16_t *act0 = nullptr, *act1 = nullptr, *stem_out = nullptr, *xn = nullptr, *o = nullptr, *hbuf = nullptr,
            *cbuf = nullptr;
   float *slab = nullptr, *x = nullptr, *qkv = nullptr, *hh = nullptr;
@@ -121,6 +130,7 @@ uint16_t to16(int dtype, float f) { return dtype == 0 ? fac_host::f32_to_bf16(f)
 // Split-K factor of the patch embedding (K = 25088 = 392 k-tiles of 64).  Fixed,
 // so a crop's logits are bit-identical whatever batch it is scored in.
 constexpr int kPatchSplits = 14;
+constexpr int kProjSplits = 4;  // split-K of the to_out / FF2 projections
 int patch_splits(int) { return kPatchSplits; }
 
 struct WsLayout {
@@ -131,7 +141,7 @@ WsLayout layout(int B, int chunk) {
   auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
   WsLayout L{};
   const int cb = (chunk > 0 && chunk < B) ? chunk : B;
-  const size_t S = (size_t)kPatchSplits * B;
+  const size_t S = (size_t)std::max(kPatchSplits, 2 * kProjSplits) * B;
   size_t off = 0;
   L.act = off; off += 2 * al((size_t)cb * kImg * kImg * 32 * 2);
   L.stem = off; off += al((size_t)B * kPatchDim * 2);
@@ -370,14 +380,29 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     const int nb = std::min(chunk, B - b0);
     const void* src = u8 ? (const void*)((const uint8_t*)in + (size_t)b0 * kImg * kImg * 3)
                          : (const void*)((const float*)in + (size_t)b0 * 3 * kImg * kImg);
-    HIP_TRY(c, launch_conv1(dt, u8, src, c->conv1_w, c->conv1_b, c->act0, nb, kImg, kImg, st));
-    MARK();
     uint16_t *cur = c->act0, *nxt = c->act1;
-    if (stop_after == 0) {
-      HIP_TRY(c, hipMemcpyAsync(feat_out, cur, (size_t)nb * kImg * kImg * 32 * 2, hipMemcpyDeviceToDevice, st));
-      return FAC_OK;
+    int l0 = 0;
+    if (c->fuse_stem224 && (stop_after < 0 || stop_after >= 2)) {
+      // conv1..conv3 + pool in one kernel; the profile reports it as stage conv1
+      HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_w, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
+                                c->conv[1].b, cur, nb, c->num_cu, st));
+      MARK();
+      MARK();
+      MARK();
+      l0 = 2;
+      if (stop_after == 2) {
+        HIP_TRY(c, hipMemcpyAsync(feat_out, cur, (size_t)nb * 112 * 112 * 32 * 2, hipMemcpyDeviceToDevice, st));
+        return FAC_OK;
+      }
+    } else {
+      HIP_TRY(c, launch_conv1(dt, u8, src, c->conv1_w, c->conv1_b, c->act0, nb, kImg, kImg, st));
+      MARK();
+      if (stop_after == 0) {
+        HIP_TRY(c, hipMemcpyAsync(feat_out, cur, (size_t)nb * kImg * kImg * 32 * 2, hipMemcpyDeviceToDevice, st));
+        return FAC_OK;
+      }
     }
-    for (int l = 0; l < 16; ++l) {
+    for (int l = l0; l < 16; ++l) {
       const ConvLayer& L = c->conv[l];
       uint16_t* dst = (l == 15) ? c->stem_out + (size_t)b0 * kPatchDim : nxt;
       HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, nb, L.H, L.H, L.Cin, L.Cout, L.pool, st));
@@ -397,18 +422,26 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   MARK();
   const int R = 2 * B;
   const float scale = 1.0f / std::sqrt((float)kDim);  // dim ** -0.5 (cvit.py:38), not head_dim
+  // The two N=1024 projections (to_out, FF2) run split-K into fp32 partial
+  // slabs; the following kernel (residual add + next LayerNorm, or the CLS
+  // finish after the last layer) sums them in split order.
+  constexpr int SK = kProjSplits;
   for (int l = 0; l < kDepth; ++l) {
     const TLayer& T = c->tl[l];
-    HIP_TRY(c, launch_layernorm(dt, c->x, T.ln1_g, T.ln1_b, c->xn, R, st));
+    if (l == 0) {
+      HIP_TRY(c, launch_layernorm(dt, c->x, T.ln1_g, T.ln1_b, c->xn, R, st));
+    } else {
+      HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, c->tl[l - 1].b2, T.ln1_g, T.ln1_b, c->xn, R, st));
+    }
     HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st));
     HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
-    HIP_TRY(c, launch_gemm(dt, EPI_RESID, c->o, kDim, T.wo, kDim, T.bo, c->x, kDim, R, kDim, kDim, 1, st));
-    HIP_TRY(c, launch_layernorm(dt, c->x, T.ln2_g, T.ln2_b, c->xn, R, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st));
+    HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, T.bo, T.ln2_g, T.ln2_b, c->xn, R, st));
     HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st));
-    HIP_TRY(c, launch_gemm(dt, EPI_RESID, c->hbuf, kMlp, T.w2, kMlp, T.b2, c->x, kDim, R, kDim, kMlp, 1, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->hbuf, kMlp, T.w2, kMlp, nullptr, c->slab, kDim, R, kDim, kMlp, SK, st));
   }
   MARK();
-  HIP_TRY(c, launch_gather_cls(dt, c->x, c->cbuf, B, st));
+  HIP_TRY(c, launch_resid_cls(dt, c->x, c->slab, SK, c->tl[kDepth - 1].b2, c->cbuf, B, st));
   HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, c->hh, kMlp, B, kMlp, kDim, 1, st));
   HIP_TRY(c, launch_head_out(c->hh, c->h2_w, c->h2_b, logits, probs, B, st));
   MARK();
@@ -427,6 +460,9 @@ int fac_create(int device, int dtype, fac_ctx** out) {
   fac_ctx* c = new fac_ctx();
   c->device = device;
   c->dtype = dtype;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    c->num_cu = ncu;
   *out = c;
   return FAC_OK;
 }
@@ -464,6 +500,17 @@ int fac_set_stem_chunk(fac_ctx* c, int crops) {
     }
   }
   return FAC_OK;
+}
+
+int fac_set_option(fac_ctx* c, const char* key, int value) {
+  if (!c || !key) return FAC_ERR_ARG;
+  const std::string k(key);
+  if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
+  if (k == "fuse_stem224") {
+    c->fuse_stem224 = value != 0;
+    return FAC_OK;
+  }
+  return set_err(c, FAC_ERR_ARG, "unknown option " + k);
 }
 
 int fac_forward_nchw_f32(fac_ctx* c, const float* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,

@@ -1,0 +1,322 @@
+// Fused 224x224 block of the conv stem: conv1 (3->32) -> conv2 (32->32) ->
+// conv3 (32->32) -> MaxPool2d(2,2), each conv with folded BN + ReLU
+// (CViT-main/model/cvit.py:88-97), plus the input normalisation of
+// cvit_prediction.py:41-45,214-215 fused into conv1's staging.
+//
+// Unfused, this block moves ~13 MB per crop through HBM (three 224x224x32
+// activations written and read back); fused, a crop costs its 150 KB of
+// uint8 pixels in and 0.8 MB of pooled 112x112x32 out.
+//
+// One persistent 512-thread workgroup per CU keeps all three weight tensors
+// in LDS (40 KB) and walks 16x16 output boxes.  Per box:
+//   A: normalised input over the 22x22 region (conv1's receptive field);
+//   B: conv1 over the 20x20 region conv2 needs -> LDS image c1;
+//   C: conv2 over the 18x18 region conv3 needs -> LDS image c2;
+//   D: conv3 over the 16x16 box, 2x2 max in registers -> 8x8x32 tile out.
+// Intermediate pixels that fall outside the image are stored as 0, which is
+// exactly the zero padding the next conv expects.  Recompute overhead:
+// conv1 x1.56, conv2 x1.27 (conv1 is 0.7% of the network's FLOPs).
+//
+// conv1 and conv2 run "transposed" (C^T = W . X^T: MFMA rows = channels,
+// cols = pixels), so each lane ends with 4 consecutive channels of one pixel
+// and writes them to the chunk-major LDS image with one 8-byte store.
+// conv3 runs in the normal orientation, where the window-major pixel order
+// puts a whole 2x2 pooling window in one lane's 4 accumulators.
+#include "common.hpp"
+
+namespace fac {
+
+template <int TW>
+__device__ __forceinline__ void win_pixel(int m, int& py, int& px) {
+  constexpr int WW = TW / 2;
+  const int w = m >> 2, sub = m & 3;
+  const int wy = w / WW, wx = w - wy * WW;
+  py = 2 * wy + (sub >> 1);
+  px = 2 * wx + (sub & 1);
+}
+
+constexpr float kNormMean[3] = {0.485f, 0.456f, 0.406f};  // cvit_prediction.py:41
+constexpr float kNormStd[3] = {0.229f, 0.224f, 0.225f};   // cvit_prediction.py:42
+
+template <class T, bool U8>
+__global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__ in_,
+                                                        const uint16_t* __restrict__ w1g,
+                                                        const float* __restrict__ b1,
+                                                        const uint16_t* __restrict__ w2g,
+                                                        const float* __restrict__ b2,
+                                                        const uint16_t* __restrict__ w3g,
+                                                        const float* __restrict__ b3,
+                                                        uint16_t* __restrict__ out, int ntiles) {
+  constexpr int IMG = 224, TPR = 14, TPI = 196;   // 16x16 boxes per row / per image
+  constexpr int RP = 24;                          // LDS image row pitch (16-byte units, == 8 mod 16)
+  constexpr int P1 = 20 * RP + 8, P2 = 18 * RP + 8;  // plane pitches of c1 / c2 (simulated: 1.33-way / 1-way)
+  constexpr int W1P = 72;                         // conv1 weight row pitch (elements)
+  constexpr int WSZ = 9 * 4 * 32 * 8;             // conv2/3 weights: [tap][q][32][8]
+  constexpr int OFF_W2 = 32 * W1P, OFF_W3 = OFF_W2 + WSZ, OFF_C1 = OFF_W3 + WSZ;
+  constexpr int OFF_C2 = OFF_C1 + 4 * P1 * 8;
+  constexpr int OFF_LUT = OFF_C2 + 4 * P2 * 8;    // u8 -> normalised 16-bit value, per channel
+  constexpr int SMEM = OFF_LUT + 3 * 256;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+  uint16_t* const sw1 = smem;
+  uint16_t* const sw2 = smem + OFF_W2;
+  uint16_t* const sw3 = smem + OFF_W3;
+  uint16_t* const c1 = smem + OFF_C1;
+  uint16_t* const c2 = smem + OFF_C2;
+  uint16_t* const lut = smem + OFF_LUT;
+  uint16_t* const sin = c2;    // 22x22x4 input image: dead before conv2 writes c2
+  uint16_t* const ostg = c1;   // 64 x (32+8) pooled tile: c1 is dead after conv2
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  for (int i = tid; i < 32 * 8; i += 512)
+    *(u16x8*)(sw1 + (i >> 3) * W1P + (i & 7) * 8) = *(const u16x8*)(w1g + i * 8);
+  for (int i = tid; i < WSZ / 8; i += 512) {
+    *(u16x8*)(sw2 + i * 8) = *(const u16x8*)(w2g + i * 8);
+    *(u16x8*)(sw3 + i * 8) = *(const u16x8*)(w3g + i * 8);
+  }
+  // The normalisation (x/255 - mean_c)/std_c of every possible uint8 value,
+  // evaluated once with the reference's IEEE fp32 ops: staging is a lookup.
+  if constexpr (U8) {
+    for (int i = tid; i < 3 * 256; i += 512) {
+      const int c = i >> 8, v = i & 255;
+      lut[i] = T::from_f32(((float)v / 255.0f - kNormMean[c]) / kNormStd[c]);
+    }
+  }
+  // Accumulators start at the folded-BN bias of the channels they hold
+  // (conv1/conv2 transposed: channel 16ct + 4g + j; conv3: 16ct + r16).
+  f32x4 bt1[2], bt2[2], bn3[2];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bt1[ct][j] = b1[ct * 16 + 4 * g + j];
+      bt2[ct][j] = b2[ct * 16 + 4 * g + j];
+    }
+    bn3[ct] = (f32x4)b3[ct * 16 + r16];
+  }
+  // Tile-invariant LDS offsets of this lane's rows in each stage.
+  int in_off[4][2], c1_wr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // conv1: row tiles wave + 8i (< 25), raster over 20x20
+    const int rt = wave + 8 * i;
+    const int m = (rt < 25 ? rt : 0) * 16 + r16;
+    const int cy = m / 20, cx = m - (m / 20) * 20;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int t = ks * 8 + 2 * g;  // taps t, t+1 (t+1 <= 9 only when t < 8)
+      in_off[i][ks] = ((cy + t / 3) * 22 + cx + t % 3) * 4;
+    }
+    c1_wr[i] = ((g >> 1) * P1 + cy * RP + cx) * 8 + (g & 1) * 4;  // + ct*2*P1*8 (channels 16ct+4g..)
+  }
+  int c2_rd[3], c2_wr[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {  // conv2: row tiles wave + 8i (< 21), window-major over 18x18
+    int m = (wave + 8 * i) * 16 + r16;
+    if (m >= 324) m = 0;
+    int py, px;
+    win_pixel<18>(m, py, px);
+    c2_rd[i] = (g * P1 + py * RP + px) * 8;
+    c2_wr[i] = ((g >> 1) * P2 + py * RP + px) * 8 + (g & 1) * 4;
+  }
+  int c3_rd[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // conv3: row tiles 2*wave + i, window-major over 16x16
+    int py, px;
+    win_pixel<16>((wave * 2 + i) * 16 + r16, py, px);
+    c3_rd[i] = (g * P2 + py * RP + px) * 8;
+  }
+
+  // Raw input pixels of a box's 22x22 receptive field, fetched one box ahead
+  // (during conv2/conv3 of the previous box) so phase A never waits on HBM.
+  float raw0 = 0.f, raw1 = 0.f, raw2 = 0.f;  // U8: the byte values; F32: normalised floats
+  bool raw_in = false;
+  auto fetch = [&](int tile) {
+    raw0 = raw1 = raw2 = 0.f;
+    raw_in = false;
+    if (tid >= 484 || tile >= ntiles) return;
+    const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
+    const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
+    const int iy = tid / 22, ix = tid - (tid / 22) * 22;
+    const int y = ty * 16 - 3 + iy, x = tx * 16 - 3 + ix;
+    if (y < 0 || y >= IMG || x < 0 || x >= IMG) return;
+    raw_in = true;
+    if constexpr (U8) {
+      const uint8_t* src = (const uint8_t*)in_ + (((size_t)b * IMG + y) * IMG + x) * 3;
+      raw0 = (float)src[0];
+      raw1 = (float)src[1];
+      raw2 = (float)src[2];
+    } else {
+      const float* src = (const float*)in_ + (size_t)b * 3 * IMG * IMG + (size_t)y * IMG + x;
+      raw0 = src[0];
+      raw1 = src[IMG * IMG];
+      raw2 = src[2 * IMG * IMG];
+    }
+  };
+  fetch(blockIdx.x);
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
+    const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
+    const int y0 = ty * 16, x0 = tx * 16;
+    __syncthreads();  // previous tile's readers of sin(=c2) and ostg(=c1) are done
+
+    // ---- A: normalised 16-bit input over (y0-3 .. y0+18) x (x0-3 .. x0+18);
+    // out-of-image pixels were fetched as 0 (zero padding in normalised space)
+    if (tid < 484) {
+      u16x4 h;
+      if constexpr (U8) {
+        h[0] = raw_in ? lut[(int)raw0] : (uint16_t)0;
+        h[1] = raw_in ? lut[256 + (int)raw1] : (uint16_t)0;
+        h[2] = raw_in ? lut[512 + (int)raw2] : (uint16_t)0;
+      } else {
+        h[0] = T::from_f32(raw0);
+        h[1] = T::from_f32(raw1);
+        h[2] = T::from_f32(raw2);
+      }
+      h[3] = 0;
+      *(u16x4*)(sin + tid * 4) = h;
+    }
+    __syncthreads();
+    // interior boxes (no receptive field pixel outside the image) skip the zeroing
+    const bool interior = ty > 0 && ty < TPR - 1 && tx > 0 && tx < TPR - 1;
+
+    // ---- B: conv1 over the 20x20 region at (y0-2, x0-2): 25 row tiles, raster order
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rt = wave + 8 * i;
+      if (rt >= 25) break;
+      f32x4 acc[2] = {bt1[0], bt1[1]};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int t0 = ks * 8 + 2 * g;
+        u16x4 lo = (u16x4)0, hi = (u16x4)0;
+        if (t0 < 9) lo = *(const u16x4*)(sin + in_off[i][ks]);
+        if (t0 + 1 < 9) hi = *(const u16x4*)(sin + in_off[i][ks] + ((t0 + 1) % 3 == 0 ? 22 * 4 - 2 * 4 : 4));
+        const u16x8 p = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const u16x8 wf = *(const u16x8*)(sw1 + (ct * 16 + r16) * W1P + ks * 32 + g * 8);
+          acc[ct] = T::mfma(wf, p, acc[ct]);
+        }
+      }
+      bool inside = true;
+      if (!interior) {
+        const int m = rt * 16 + r16;
+        const int cy = m / 20, cx = m - (m / 20) * 20;
+        inside = (unsigned)(y0 - 2 + cy) < (unsigned)IMG && (unsigned)(x0 - 2 + cx) < (unsigned)IMG;
+      }
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        u16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = T::from_f32(fmaxf(acc[ct][j], 0.f));
+        if (!inside) o = (u16x4)0;
+        *(u16x4*)(c1 + c1_wr[i] + ct * 2 * P1 * 8) = o;
+      }
+    }
+    __syncthreads();
+
+    fetch(tile + gridDim.x);  // next box's pixels land while conv2/conv3 run
+
+    // ---- C: conv2 over the 18x18 region at (y0-1, x0-1): window-major, 21 row tiles
+    {
+      f32x4 acc[3][2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        acc[i][0] = bt2[0];
+        acc[i][1] = bt2[1];
+      }
+      const bool has3 = wave + 16 < 21;  // waves 0-4 own three row tiles, 5-7 two
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = ((t / 3) * RP + (t % 3)) * 8;
+        u16x8 wf[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw2 + ((t * 4 + g) * 32 + ct * 16 + r16) * 8);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          if (i == 2 && !has3) continue;
+          const u16x8 a = *(const u16x8*)(c1 + c2_rd[i] + toff);
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(wf[ct], a, acc[i][ct]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        if (i == 2 && !has3) continue;
+        const int m = (wave + 8 * i) * 16 + r16;
+        bool keep = m < 324;
+        if (!interior && keep) {
+          int py, px;
+          win_pixel<18>(m, py, px);
+          keep = (unsigned)(y0 - 1 + py) < (unsigned)IMG && (unsigned)(x0 - 1 + px) < (unsigned)IMG;
+        }
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          u16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = T::from_f32(fmaxf(acc[i][ct][j], 0.f));
+          if (!keep) o = (u16x4)0;
+          if (m < 324) *(u16x4*)(c2 + c2_wr[i] + ct * 2 * P2 * 8) = o;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- D: conv3 over the 16x16 box, window-major, 2x2 max-pool in registers
+    {
+      f32x4 acc[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc[i][0] = bn3[0];
+        acc[i][1] = bn3[1];
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = ((t / 3) * RP + (t % 3)) * 8;
+        u16x8 wf[2];
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw3 + ((t * 4 + g) * 32 + ct * 16 + r16) * 8);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const u16x8 a = *(const u16x8*)(c2 + c3_rd[i] + toff);
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(a, wf[ct], acc[i][ct]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const f32x4 v = acc[i][ct];
+          const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+          ostg[((wave * 2 + i) * 4 + g) * 40 + ct * 16 + r16] = T::from_f32(fmaxf(mx, 0.f));
+        }
+    }
+    __syncthreads();
+    if (tid < 256) {
+      const int w = tid >> 2, q = tid & 3;
+      const int wy = w >> 3, wx = w & 7;
+      *(u16x8*)(out + (((size_t)b * 112 + (y0 >> 1) + wy) * 112 + (x0 >> 1) + wx) * 32 + q * 8) =
+          *(const u16x8*)(ostg + w * 40 + q * 8);
+    }
+  }
+}
+
+hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
+                          const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
+                          hipStream_t st) {
+  const int ntiles = B * 196;
+  const int grid = nwg < ntiles ? nwg : ntiles;
+  if (dtype == 0) {
+    if (u8) stem224_fused<BF16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
+    else stem224_fused<BF16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
+  } else {
+    if (u8) stem224_fused<F16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
+    else stem224_fused<F16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fac

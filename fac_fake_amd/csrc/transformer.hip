@@ -20,53 +20,57 @@ enum GemmEpi : int {
 };
 
 // 64x64 output tile, BK = 64, 4 waves in a 2x2 grid (32x32 each = 2x2 MFMA
-// 16x16x32 tiles), register-staged double-buffered LDS.
+// 16x16x32 tiles).  K-tiles stream through a 3-slot LDS ring: tile s is
+// fetched into register set s & 1 at the top of step s-2 and written to slot
+// s % 3 at the end of step s-1, so every fetch has two steps of MFMA work to
+// land (the per-step L2 latency was what bound these small-M GEMMs).
+// blockIdx.z selects a K range of Kper (split-K; Kper / 64 must be even).
 template <class T, int EPI>
-__global__ __launch_bounds__(256) void gemm_nt(const uint16_t* __restrict__ A, int lda,
-                                               const uint16_t* __restrict__ Wt, int ldw,
-                                               const float* __restrict__ bias, void* __restrict__ out_,
-                                               int ldo, int M, int N, int Kper) {
+__global__ __launch_bounds__(256, 2) void gemm_nt(const uint16_t* __restrict__ A, int lda,
+                                                  const uint16_t* __restrict__ Wt, int ldw,
+                                                  const float* __restrict__ bias, void* __restrict__ out_,
+                                                  int ldo, int M, int N, int Kper) {
   constexpr int BM = 64, BN = 64, BK = 64, PS = BK + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (BM + BN) * PS];
+  constexpr int SLOT = (BM + BN) * PS;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[3 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int k0 = blockIdx.z * Kper;
   const int nkt = Kper / BK;
 
-  u16x8 ra[2], rb[2];
-  auto load = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int it = tid + 256 * i;
-      const int r = it >> 3, q = it & 7;
-      const int m = m0 + r;
-      ra[i] = (m < M) ? *(const u16x8*)(A + (size_t)m * lda + k0 + kt * BK + q * 8) : (u16x8)0;
-      rb[i] = *(const u16x8*)(Wt + (size_t)(n0 + r) * ldw + k0 + kt * BK + q * 8);
-    }
+  // per-thread staging coordinates: rows r0, r0+32 of both tiles, 16-byte piece q
+  const int r0 = tid >> 3, q = tid & 7;
+  const bool va0 = m0 + r0 < M, va1 = m0 + r0 + 32 < M;
+  const uint16_t* pa0 = A + (size_t)(va0 ? m0 + r0 : 0) * lda + k0 + q * 8;
+  const uint16_t* pa1 = A + (size_t)(va1 ? m0 + r0 + 32 : 0) * lda + k0 + q * 8;
+  const uint16_t* pb0 = Wt + (size_t)(n0 + r0) * ldw + k0 + q * 8;
+  const uint16_t* pb1 = Wt + (size_t)(n0 + r0 + 32) * ldw + k0 + q * 8;
+  const int so0 = r0 * PS + q * 8, so1 = (r0 + 32) * PS + q * 8;
+
+  u16x8 rg[2][4];
+  auto load = [&](u16x8* r, int kt) {
+    const int ko = kt * BK;
+    r[0] = va0 ? *(const u16x8*)(pa0 + ko) : (u16x8)0;
+    r[1] = va1 ? *(const u16x8*)(pa1 + ko) : (u16x8)0;
+    r[2] = *(const u16x8*)(pb0 + ko);
+    r[3] = *(const u16x8*)(pb1 + ko);
   };
-  auto store = [&](int buf) {
-    uint16_t* sa = smem + buf * (BM + BN) * PS;
+  auto store = [&](const u16x8* r, int slot) {
+    uint16_t* sa = smem + slot * SLOT;
     uint16_t* sb = sa + BM * PS;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int it = tid + 256 * i;
-      const int r = it >> 3, q = it & 7;
-      *(u16x8*)(sa + r * PS + q * 8) = ra[i];
-      *(u16x8*)(sb + r * PS + q * 8) = rb[i];
-    }
+    *(u16x8*)(sa + so0) = r[0];
+    *(u16x8*)(sa + so1) = r[1];
+    *(u16x8*)(sb + so0) = r[2];
+    *(u16x8*)(sb + so1) = r[3];
   };
 
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = (f32x4)0.f;
 
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) load(kt + 1);
-    const uint16_t* sa = smem + (kt & 1) * (BM + BN) * PS;
+  auto compute = [&](int slot) {
+    const uint16_t* sa = smem + slot * SLOT;
     const uint16_t* sb = sa + BM * PS;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
@@ -81,7 +85,26 @@ __global__ __launch_bounds__(256) void gemm_nt(const uint16_t* __restrict__ A, i
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
     }
-    if (kt + 1 < nkt) store((kt + 1) & 1);
+  };
+
+  load(rg[0], 0);
+  if (nkt > 1) load(rg[1], 1);
+  store(rg[0], 0);
+  __syncthreads();
+  int slot = 0;
+  for (int kt = 0; kt < nkt; kt += 2) {
+    // step kt (register set 0 free: its tile was stored at the end of step kt-1)
+    if (kt + 2 < nkt) load(rg[0], kt + 2);
+    compute(slot);
+    slot = slot == 2 ? 0 : slot + 1;
+    if (kt + 1 < nkt) store(rg[1], slot);
+    __syncthreads();
+    if (kt + 1 >= nkt) break;
+    // step kt+1 (register set 1 free)
+    if (kt + 3 < nkt) load(rg[1], kt + 3);
+    compute(slot);
+    slot = slot == 2 ? 0 : slot + 1;
+    if (kt + 2 < nkt) store(rg[0], slot);
     __syncthreads();
   }
 
@@ -139,8 +162,7 @@ __global__ __launch_bounds__(256) void embed_finalize(const float* __restrict__ 
 }
 
 // LayerNorm(1024, eps 1e-5) (PreNorm, cvit.py:13-20): one wave per row,
-// fp32 statistics, 16-bit output feeding the next GEMM.  With `stride2` the
-// kernel reads only rows 0, 2, 4... (the CLS rows) and skips the affine.
+// fp32 statistics, 16-bit output feeding the next GEMM.
 template <class T>
 __global__ __launch_bounds__(256) void layernorm_rows(const float* __restrict__ x, const float* __restrict__ g,
                                                       const float* __restrict__ bta, uint16_t* __restrict__ y,
@@ -174,6 +196,66 @@ __global__ __launch_bounds__(256) void layernorm_rows(const float* __restrict__ 
     for (int j = 0; j < 4; ++j) o[j] = T::from_f32((v[i][j] - mean) * rstd * g[c + j] + bta[c + j]);
     *(u16x4*)(y + (size_t)row * 1024 + c) = o;
   }
+}
+
+// Residual add of a split-K projection + the next PreNorm LayerNorm, fused:
+//   x[r] += (sum_s slab[s][r]) + bias      (Residual, cvit.py:10-11)
+//   y[r]  = LayerNorm(x[r]) * g + b -> 16-bit (PreNorm, cvit.py:19-20)
+// The partial sums are added in split order: deterministic, no atomics.
+template <class T>
+__global__ __launch_bounds__(256) void resid_layernorm(float* __restrict__ x, const float* __restrict__ slab, int S,
+                                                       const float* __restrict__ bias, const float* __restrict__ g,
+                                                       const float* __restrict__ bta, uint16_t* __restrict__ y,
+                                                       int R) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= R) return;
+  float* xr = x + (size_t)row * 1024;
+  f32x4 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = i * 256 + lane * 4;
+    f32x4 p = *(const f32x4*)(slab + (size_t)row * 1024 + c);
+    for (int k = 1; k < S; ++k) p += *(const f32x4*)(slab + ((size_t)k * R + row) * 1024 + c);
+    v[i] = (p + *(const f32x4*)(bias + c)) + *(const f32x4*)(xr + c);
+    *(f32x4*)(xr + c) = v[i];
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+  const float mean = wave_sum(s) * (1.0f / 1024.0f);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float d = v[i][j] - mean;
+      q += d * d;
+    }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / 1024.0f) + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = i * 256 + lane * 4;
+    u16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = T::from_f32((v[i][j] - mean) * rstd * g[c + j] + bta[c + j]);
+    *(u16x4*)(y + (size_t)row * 1024 + c) = o;
+  }
+}
+
+// After the last layer only the CLS rows matter (cvit.py:177): finish their
+// residual add from the FF2 split-K partials and convert to 16-bit for the head.
+template <class T>
+__global__ __launch_bounds__(256) void resid_cls(const float* __restrict__ x, const float* __restrict__ slab, int S,
+                                                 const float* __restrict__ bias, uint16_t* __restrict__ c, int B) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // over B*256 float4 groups
+  if (i >= B * 256) return;
+  const int b = i >> 8, col = (i & 255) * 4, row = 2 * b, R = 2 * B;
+  f32x4 p = *(const f32x4*)(slab + (size_t)row * 1024 + col);
+  for (int k = 1; k < S; ++k) p += *(const f32x4*)(slab + ((size_t)k * R + row) * 1024 + col);
+  const f32x4 v = (p + *(const f32x4*)(bias + col)) + *(const f32x4*)(x + (size_t)row * 1024 + col);
+  u16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = T::from_f32(v[j]);
+  *(u16x4*)(c + (size_t)b * 1024 + col) = o;
 }
 
 // CLS rows of the fp32 residual stream -> 16-bit [B][1024] (cvit.py:177).
@@ -311,7 +393,7 @@ static hipError_t launch_gemm_t(int epi, const uint16_t* A, int lda, const uint1
 
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
                        void* out, int ldo, int M, int N, int K, int splits, hipStream_t st) {
-  if (N % 64 != 0 || K % (64 * splits) != 0) return hipErrorInvalidValue;
+  if (N % 64 != 0 || K % (128 * splits) != 0) return hipErrorInvalidValue;  // Kper: even number of 64-wide tiles
   if (dtype == 0) return launch_gemm_t<BF16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, st);
   return launch_gemm_t<F16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, st);
 }
@@ -327,6 +409,22 @@ hipError_t launch_layernorm(int dtype, const float* x, const float* g, const flo
   dim3 grid((R + 3) / 4);
   if (dtype == 0) layernorm_rows<BF16><<<grid, 256, 0, st>>>(x, g, b, y, R);
   else layernorm_rows<F16><<<grid, 256, 0, st>>>(x, g, b, y, R);
+  return hipGetLastError();
+}
+
+hipError_t launch_resid_layernorm(int dtype, float* x, const float* slab, int S, const float* bias, const float* g,
+                                 const float* b, uint16_t* y, int R, hipStream_t st) {
+  dim3 grid((R + 3) / 4);
+  if (dtype == 0) resid_layernorm<BF16><<<grid, 256, 0, st>>>(x, slab, S, bias, g, b, y, R);
+  else resid_layernorm<F16><<<grid, 256, 0, st>>>(x, slab, S, bias, g, b, y, R);
+  return hipGetLastError();
+}
+
+hipError_t launch_resid_cls(int dtype, const float* x, const float* slab, int S, const float* bias, uint16_t* c, int B,
+                            hipStream_t st) {
+  dim3 grid(B);
+  if (dtype == 0) resid_cls<BF16><<<grid, 256, 0, st>>>(x, slab, S, bias, c, B);
+  else resid_cls<F16><<<grid, 256, 0, st>>>(x, slab, S, bias, c, B);
   return hipGetLastError();
 }
 

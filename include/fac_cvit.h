@@ -86,10 +86,12 @@ int fac_forward_nhwc_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t*
 /* Test/measurement entry points ------------------------------------------
  * fac_debug_features_u8: run conv1..conv{layer+1} (layer 0..16) on uint8
  * crops and copy that block's NHWC 16-bit output (after ReLU, and after the
- * MaxPool where one follows) to d_out.  For per-layer parity tests.
+ * MaxPool where one follows) to d_out.  For per-layer parity tests; layers
+ * 0 and 1 always use the unfused conv1/conv2 kernels.
  * fac_profile_forward_u8: one forward with a hipEvent between stages;
  * synchronises and writes FAC_PROFILE_STAGES durations (ms): conv1..conv17,
- * patch embedding, transformer (6 layers), head.
+ * patch embedding, transformer (6 layers), head.  With the fused 224 block
+ * its whole time is stage conv1 and conv2/conv3 read 0.
  * fac_debug_conv: run stem conv `layer` (1..16 = conv2..conv17) alone on a
  * given NHWC 16-bit input.  fac_debug_tail: patch embedding + transformer +
  * head from a given NHWC 16-bit stem output [B,7,7,512]. */
@@ -112,6 +114,10 @@ int fac_video_score(const float* d_logits, int n, float* d_score, void* stream);
 /* Tuning knob: run the conv stem in sub-batches of `crops` crops (0 = whole
  * batch), so intermediate activations stay resident in the Infinity Cache. */
 int fac_set_stem_chunk(fac_ctx* ctx, int crops);
+
+/* Named knobs: "stem_chunk" (as above), "fuse_stem224" (1 = conv1..conv3 +
+ * pool as one fused kernel, the default; 0 = one kernel per conv). */
+int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);
 void fac_destroy(fac_ctx* ctx);
