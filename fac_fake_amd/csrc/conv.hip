@@ -15,6 +15,8 @@
 // 2x2 pooling window), so in the 16x16x32 MFMA C layout (row = 4*(lane>>4) +
 // reg) each lane holds a whole window of one channel: the 2x2 max-pool is
 // three fmaxf in registers.
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace fac {
@@ -31,6 +33,13 @@ constexpr int CONV_CK = 32;  // input channels per K chunk (= 4 x 16-byte "q" pi
 //  * weight slice: q-major [q][BN], identical to its global packing
 //    [n-block][chunk][tap][q][BN][8], so staging is a linear 16-byte copy and
 //    B-fragment reads are conflict-free.
+// Async global -> LDS copy of 16 bytes per lane (global_load_lds_dwordx4): the
+// wave's 64 pieces land contiguously at the wave-uniform LDS address `ldst`.
+__device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
+}
+
 template <int TW>
 constexpr int halo_rp() { return TW + 2 <= 24 ? 24 : 40; }
 
@@ -71,7 +80,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
-                                                       int Cin, int Cout) {
+                                                       int Cin, int Cout, const uint16_t* __restrict__ zero16) {
   constexpr int CK = CONV_CK;
   constexpr int HH = TH + 2, HWD = TW + 2;
   constexpr int HALO_RP = halo_rp<TW>();
@@ -80,17 +89,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
   constexpr int RT = ((NPIX + 15) / 16 + WM - 1) / WM * WM;
   constexpr int RTW = RT / WM;
   constexpr int CTW = BN / 16 / WN;
-  constexpr int HALO = 4 * NHP * 8;         // elements per halo buffer
+  // The halo image is filled by global_load_lds, one 64-slot wave
+  // instruction at a time; pad it to whole instructions, a multiple of 4 so
+  // every wave issues the same number (HPW).
+  constexpr int HSLOTS = (4 * NHP + 255) / 256 * 256;
+  constexpr int HPW = HSLOTS / 256;
+  constexpr int HALO = HSLOTS * 8;          // elements per halo buffer
   constexpr int WSL = BN * CK;              // elements per tap slice
   constexpr int OPIX = POOL ? NPIX / 4 : NPIX;
   constexpr int OPS = BN + 8;
   constexpr int OPER = 2 * HALO + 3 * WSL;           // halo double buffer + 3-slot weight ring
   constexpr int OSTG = (POOL ? RT * 4 : RT * 16) * OPS;  // padded: epilogue writes unguarded
   constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
-  constexpr int HITEMS = HH * HWD * 4;
-  constexpr int HLOADS = (HITEMS + 255) / 256;
-  constexpr int WITEMS = BN * 4;
-  constexpr int WLOADS = (WITEMS + 255) / 256;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(TH % 2 == 0 && TW % 2 == 0, "window-major order needs even boxes");
   static_assert(CTW * 16 * WN == BN, "BN split");
@@ -108,47 +118,38 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
   const uint16_t* in_b = in + (size_t)b * H * W * Cin;
   const uint16_t* wsrc = wpk + (size_t)nb * nchunks * 9 * WSL;
 
-  // Halo staging map, fixed across chunks: element offset of each of this
-  // thread's 16-byte pieces in the image (-1 = zero padding / unused) and its
-  // place in the LDS image (-1 = unused).
-  int hsrc[HLOADS], hdst[HLOADS];
+  // Halo staging map, fixed across chunks: each lane of each halo glds
+  // instruction owns one 16-byte slot of the LDS image (plane q, row hy,
+  // column hx); it copies that piece of the image, or 16 zero bytes for
+  // zero padding / pitch padding (a pointer that does not move with c).
+  int hsrc[HPW];
 #pragma unroll
-  for (int i = 0; i < HLOADS; ++i) {
-    const int it = tid + 256 * i;
+  for (int i = 0; i < HPW; ++i) {
+    const int slot = (i * 4 + wave) * 64 + lane;
+    const int q = slot / NHP, j = slot - (slot / NHP) * NHP;
+    const int hy = j / HALO_RP, hx = j - (j / HALO_RP) * HALO_RP;
+    const int y = y0 + hy - 1, x = x0 + hx - 1;
     hsrc[i] = -1;
-    hdst[i] = -1;
-    if (it < HITEMS) {
-      const int p = it >> 2, q = it & 3;
-      const int hy = p / HWD, hx = p - (p / HWD) * HWD;
-      const int y = y0 + hy - 1, x = x0 + hx - 1;
-      if (y >= 0 && y < H && x >= 0 && x < W) hsrc[i] = (y * W + x) * Cin + q * 8;
-      hdst[i] = (q * NHP + hy * HALO_RP + hx) * 8;
-    }
+    if (q < 4 && hy < HH && hx < HWD && y >= 0 && y < H && x >= 0 && x < W) hsrc[i] = (y * W + x) * Cin + q * 8;
   }
-  u16x8 hreg[HLOADS];
-  u16x8 wreg[3][WLOADS];  // register sets of the weight ring (set = slot = step % 3)
-  auto load_halo = [&](int c) {
+  auto issue_halo = [&](uint16_t* dst, int c) {
 #pragma unroll
-    for (int i = 0; i < HLOADS; ++i)
-      hreg[i] = hsrc[i] >= 0 ? *(const u16x8*)(in_b + hsrc[i] + c * CK) : (u16x8)0;
-  };
-  auto store_halo = [&](uint16_t* dst) {
-#pragma unroll
-    for (int i = 0; i < HLOADS; ++i)
-      if (hdst[i] >= 0) *(u16x8*)(dst + hdst[i]) = hreg[i];
-  };
-  auto load_w = [&](u16x8* r, const uint16_t* src) {
-#pragma unroll
-    for (int i = 0; i < WLOADS; ++i) {
-      const int it = tid + 256 * i;
-      if (WITEMS % 256 == 0 || it < WITEMS) r[i] = *(const u16x8*)(src + it * 8);
+    for (int i = 0; i < HPW; ++i) {
+      const uint16_t* src = hsrc[i] >= 0 ? in_b + hsrc[i] + c * CK : zero16;
+      glds16(src, dst + (i * 4 + wave) * 64 * 8);
     }
   };
-  auto store_w = [&](const u16x8* r, uint16_t* dst) {
+  // Weight slices stream global -> LDS by global_load_lds: the packing of a
+  // slice in memory IS its LDS image, so wave w copies pieces
+  // [256i + 64w, +64) straight into ring slot `slot`.
+  constexpr int WPIECES = BN * CK / 8;
+  constexpr int WPW = (WPIECES + 255) / 256;  // glds instructions per wave per slice
+  uint16_t* const wring = smem + 2 * HALO;
+  auto issue_w = [&](int slot, const uint16_t* src) {
 #pragma unroll
-    for (int i = 0; i < WLOADS; ++i) {
-      const int it = tid + 256 * i;
-      if (WITEMS % 256 == 0 || it < WITEMS) *(u16x8*)(dst + it * 8) = r[i];
+    for (int i = 0; i < WPW; ++i) {
+      const int pb = i * 256 + wave * 64;
+      if (WPIECES % 256 == 0 || pb < WPIECES) glds16(src + (size_t)(pb + lane) * 8, wring + slot * WSL + pb * 8);
     }
   };
 
@@ -172,34 +173,34 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
     for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = (f32x4)0.f;
 
   // K loop: chunks of 32 input channels (runtime) x 9 taps (unrolled, so LDS
-  // offsets are immediates).  Weight slice s = 9c + t lives in ring slot s % 3
-  // = t % 3 (9 is a multiple of 3): it is fetched into register set s % 3 at
-  // the top of step s-2 and written to LDS at the end of step s-1, so each
-  // fetch has two steps of MFMA work to land.  The next chunk's halo is
-  // fetched at t = 0 and written at t = 8.
-  uint16_t* const wring = smem + 2 * HALO;
+  // offsets and wait counts are immediates).  Slice s = 9c + t lives in ring
+  // slot s % 3 = t % 3; it is issued (glds) at the top of step s-2, so each
+  // slice has two steps of MFMA work to land.  The wait before each barrier
+  // retires slice s+1 only - the slice issued this step (and the halo loads
+  // of t = 0, which are younger than slice s+1 at t = 0 and t = 1) stay in
+  // flight across it (cdna_hip_programming.md §5 "Pipelining across
+  // barriers": counted vmcnt + raw s_barrier, never __syncthreads here).
+  // The next chunk's halo is fetched at t = 0 and written at t = 8.
   const int nsteps = nchunks * 9;
-  load_halo(0);
-  load_w(wreg[0], wsrc);
-  if (nsteps > 1) load_w(wreg[1], wsrc + WSL);
-  wsrc += 2 * WSL;
-  store_halo(smem);
-  store_w(wreg[0], wring);
-  __syncthreads();
+  issue_w(0, wsrc);
+  issue_w(1, wsrc + WSL);
+  issue_halo(smem, 0);
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 
   for (int c = 0; c < nchunks; ++c) {
     const uint16_t* hb = smem + (c & 1) * HALO;
     const bool next_h = c + 1 < nchunks;
-    const int s0 = c * 9;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (s0 + t + 2 < nsteps) {
-        load_w(wreg[(t + 2) % 3], wsrc);
-        wsrc += WSL;
-      }
-      if (t == 0 && next_h) load_halo(c + 1);
+    const uint16_t* wnext = wsrc + (size_t)(c * 9 + 2) * WSL;
+    auto step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      // slice s+2 (past the end: a dummy re-read of slice 0 into a dead slot)
+      // issue order: slice s+2, then (t = 0) the next chunk's halo into the
+      // other halo buffer (on the last chunk a dummy re-read of this chunk);
+      // glds are LDS writes, so the compiler keeps them in program order
+      issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
+      if (t == 0) issue_halo(smem + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
       const uint16_t* wb = wring + (t % 3) * WSL;
-      const int toff = ((t / 3) * HALO_RP + (t % 3)) * 8;
+      constexpr int toff = ((t / 3) * HALO_RP + (t % 3)) * 8;
       u16x8 bfr[CTW];
 #pragma unroll
       for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
@@ -209,11 +210,25 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
 #pragma unroll
         for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(a, bfr[ct], acc[rt][ct]);
       }
-      if (s0 + t + 1 < nsteps) store_w(wreg[(t + 1) % 3], wring + ((t + 1) % 3) * WSL);
-      if (t == 8 && next_h) store_halo(smem + ((c + 1) & 1) * HALO);
-      __syncthreads();
-    }
+      // Retire slice s+1 (and at t = 8 the next halo), leaving younger glds in
+      // flight; wait + barrier in ONE asm statement, so no LDS access can be
+      // scheduled between this wave's wait and the workgroup barrier.
+      constexpr int N = WPW + (t <= 1 ? HPW : 0);
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{});
+    step(std::integral_constant<int, 7>{});
+    step(std::integral_constant<int, 8>{});
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy slices land before LDS is reused
+  __syncthreads();
 
   // Epilogue: folded-BN bias + ReLU (+ 2x2 max) -> 16-bit -> LDS -> global.
   uint16_t* ostg = smem;
@@ -370,31 +385,33 @@ int conv_block_n(int H) {
 
 template <class T, int TH, int TW, int BN, int WM, int WN>
 static void launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
-                       int Cin, int Cout, bool pool, hipStream_t st) {
+                       int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
-  if (pool) conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout);
-  else conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout);
+  if (pool)
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
+  else
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
 }
 
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
-                                int B, int H, int W, int Cin, int Cout, bool pool, hipStream_t st) {
+                                int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st) {
   if (W != H) return hipErrorInvalidValue;
   switch (H) {
-    case 224: launch_box<T, 16, 16, 32, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
-    case 112: launch_box<T, 16, 16, 64, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
-    case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
-    case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
-    case 14: launch_box<T, 14, 14, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, st); break;
+    case 224: launch_box<T, 16, 16, 32, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 112: launch_box<T, 16, 16, 64, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 14: launch_box<T, 14, 14, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
-                          int B, int H, int W, int Cin, int Cout, bool pool, hipStream_t st) {
-  if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, st);
-  return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, st);
+                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st) {
+  if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st);
+  return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st);
 }
 
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,

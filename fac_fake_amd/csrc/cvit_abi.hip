@@ -23,7 +23,7 @@
 namespace fac {
 int conv_block_n(int H);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
-                          int B, int H, int W, int Cin, int Cout, bool pool, hipStream_t st);
+                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st);
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
                         int B, int H, int W, hipStream_t st);
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
@@ -109,6 +109,7 @@ struct fac_ctx {
            *cbuf = nullptr;
   float *slab = nullptr, *x = nullptr, *qkv = nullptr, *hh = nullptr;
   int* errflag = nullptr;
+  uint16_t* zero16 = nullptr;  // 256 zero bytes: the source of zero-padding glds pieces
 };
 
 namespace {
@@ -134,7 +135,7 @@ constexpr int kProjSplits = 4;  // split-K of the to_out / FF2 projections
 int patch_splits(int) { return kPatchSplits; }
 
 struct WsLayout {
-  size_t act, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, total;
+  size_t act, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
 };
 
 WsLayout layout(int B, int chunk) {
@@ -154,6 +155,7 @@ WsLayout layout(int B, int chunk) {
   L.cbuf = off; off += al((size_t)B * kDim * 2);
   L.hh = off; off += al((size_t)B * kMlp * 4);
   L.err = off; off += 256;
+  L.zero = off; off += 256;
   L.total = off;
   return L;
 }
@@ -186,6 +188,7 @@ int ensure_ws(fac_ctx* c, int B) {
   c->cbuf = (uint16_t*)(base + L.cbuf);
   c->hh = (float*)(base + L.hh);
   c->errflag = (int*)(base + L.err);
+  c->zero16 = (uint16_t*)(base + L.zero);  // the whole workspace was just zeroed
   c->ws_bytes = L.total;
   c->cap_B = B;
   return FAC_OK;
@@ -405,7 +408,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     for (int l = l0; l < 16; ++l) {
       const ConvLayer& L = c->conv[l];
       uint16_t* dst = (l == 15) ? c->stem_out + (size_t)b0 * kPatchDim : nxt;
-      HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, nb, L.H, L.H, L.Cin, L.Cout, L.pool, st));
+      HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, nb, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st));
       MARK();
       if (stop_after == l + 1) {
         const int Ho = L.pool ? L.H / 2 : L.H;
@@ -533,7 +536,8 @@ int fac_debug_conv(fac_ctx* c, int layer, const uint16_t* d_in, int B, uint16_t*
   if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "debug_conv before fac_load_weights");
   DevGuard g(c->device);
   const ConvLayer& L = c->conv[layer - 1];
-  HIP_TRY(c, fac::launch_conv3x3(c->dtype, d_in, L.w, L.b, d_out, B, L.H, L.H, L.Cin, L.Cout, L.pool, (hipStream_t)stream));
+  HIP_TRY(c, fac::launch_conv3x3(c->dtype, d_in, L.w, L.b, d_out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16,
+                                 (hipStream_t)stream));
   return FAC_OK;
 }
 
