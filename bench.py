@@ -51,6 +51,20 @@ def conv_layer_flops(i: int, B: int) -> float:
     return 2.0 * B * H * H * co * 9 * ci
 
 
+def pmc_traffic(stage: str, dtype: str):
+    """HBM bytes per launch of `stage` from the newest committed PMC summary
+    (profiles/*_traffic.json, FETCH_SIZE/WRITE_SIZE passes, gfx950-corrected
+    by tools/rocprof_summary.py), or None when no summary covers it."""
+    files = sorted((REPO / "profiles").glob(f"*_{dtype}_traffic.json"))
+    if not files:
+        return None, None
+    try:
+        t = json.loads(files[-1].read_text()).get("by_stage", {}).get(stage)
+    except (OSError, ValueError):
+        return None, None
+    return (t["hbm_bytes"] if t else None), files[-1].name
+
+
 def cpu_baseline(sd, threads: int, iters: int = 4, batch: int = 32):
     from oracle.cvit_torch import forward_fp32, normalize_u8
     torch.set_num_threads(threads)
@@ -177,6 +191,7 @@ def main():
         dom_flops = sum(conv_layer_flops(i, B) for i in range(3))
         dom_name = "stem224_fused (conv1-conv3 + pool)"
     achieved = dom_flops / (conv_ms[dom] * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(STAGE_NAMES[dom], args.dtype)
     peak = PEAK_TFLOPS[args.dtype]
 
     value = world * B * args.steps / elapsed
@@ -202,7 +217,7 @@ def main():
         "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
         "roofline": {"bound": "mfma", "kernel": dom_name,
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "launch_ms": round(float(conv_ms[dom]), 4), "flops_per_launch": dom_flops},
         "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, acc)},
     }

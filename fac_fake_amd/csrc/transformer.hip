@@ -353,18 +353,29 @@ __global__ __launch_bounds__(256) void head_out(const float* __restrict__ hid, c
 
 // Video-level score (pre_process_prediction, cvit_prediction.py:266-281) over
 // n per-crop logit pairs: p = sigmoid(logits); if n > 2: f = mean p0,
-// r = mean p1, score = f if f > r else |1 - r|; else 0.5.  Sequential fp32
-// sums in crop order (the reference's Python sum() over 0-d tensors).
-__global__ void video_score(const float* __restrict__ logits, int n, float* __restrict__ score) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// r = mean p1, score = f if f > r else |1 - r|; else 0.5.  The sigmoids run
+// in parallel; the two sums stay sequential fp32 in crop order (the
+// reference's Python sum() over 0-d tensors), done by one lane from LDS.
+__global__ __launch_bounds__(1024) void video_score(const float* __restrict__ logits, int n,
+                                                    float* __restrict__ score) {
+  constexpr int CAP = 4096;  // crops per LDS pass
+  __shared__ float sp[2 * CAP];
+  float f = 0.f, r = 0.f;
+  for (int base = 0; base < n; base += CAP) {
+    const int m = n - base < CAP ? n - base : CAP;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * m; i += blockDim.x) sp[i] = 1.0f / (1.0f + expf(-logits[2 * base + i]));
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 0; i < m; ++i) {
+        f += sp[2 * i];
+        r += sp[2 * i + 1];
+      }
+  }
+  if (threadIdx.x != 0) return;
   if (n <= 2) {
     *score = 0.5f;
     return;
-  }
-  float f = 0.f, r = 0.f;
-  for (int i = 0; i < n; ++i) {
-    f += 1.0f / (1.0f + expf(-logits[2 * i]));
-    r += 1.0f / (1.0f + expf(-logits[2 * i + 1]));
   }
   f = f / (float)n;
   r = r / (float)n;
@@ -449,7 +460,7 @@ hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, f
 }
 
 hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st) {
-  video_score<<<1, 64, 0, st>>>(logits, n, score);
+  video_score<<<1, 1024, 0, st>>>(logits, n, score);
   return hipGetLastError();
 }
 
