@@ -105,8 +105,9 @@ struct fac_ctx {
   int stem_chunk = 0;
   int fuse_stem224 = 1;  // conv1..conv3+pool as one persistent kernel (stem224.hip)
   int num_cu = 256;
-  uint16_t *act0 = nullptr, *act1 = nullptr, *stem_out = nullptr, *xn = nullptr, *o = nullptr, *hbuf = nullptr,
-           *cbuf = nullptr;
+  uint16_t *act0 = nullptr, *act1 = nullptr, *deep0 = nullptr, *deep1 = nullptr, *stem_out = nullptr, *xn = nullptr,
+           *o = nullptr, *hbuf = nullptr, *cbuf = nullptr;
+  int cap_chunk = 0;  // crops act0/act1 hold
   float *slab = nullptr, *x = nullptr, *qkv = nullptr, *hh = nullptr;
   int* errflag = nullptr;
   uint16_t* zero16 = nullptr;  // 256 zero bytes: the source of zero-padding glds pieces
@@ -135,16 +136,26 @@ constexpr int kProjSplits = 4;  // split-K of the to_out / FF2 projections
 int patch_splits(int) { return kPatchSplits; }
 
 struct WsLayout {
-  size_t act, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
+  size_t act, deep, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
+  int cb;  // crops the high-res activation buffers hold (stem chunk)
 };
+
+// Elements per crop of the largest activation each buffer pair holds:
+// high-res stage (conv1..conv9, chunked): 224x224x32; deep stage (conv10..
+// conv17, whole batch): 28x28x256.
+constexpr size_t kActElems = (size_t)kImg * kImg * 32;
+constexpr size_t kDeepElems = (size_t)28 * 28 * 256;
+constexpr int kLastChunked = 7;  // c->conv[7] = conv9: the last conv run per stem chunk
 
 WsLayout layout(int B, int chunk) {
   auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
   WsLayout L{};
   const int cb = (chunk > 0 && chunk < B) ? chunk : B;
+  L.cb = cb;
   const size_t S = (size_t)std::max(kPatchSplits, 2 * kProjSplits) * B;
   size_t off = 0;
-  L.act = off; off += 2 * al((size_t)cb * kImg * kImg * 32 * 2);
+  L.act = off; off += 2 * al((size_t)cb * kActElems * 2);
+  L.deep = off; off += 2 * al((size_t)B * kDeepElems * 2);
   L.stem = off; off += al((size_t)B * kPatchDim * 2);
   L.slab = off; off += al(S * kDim * 4);
   L.x = off; off += al((size_t)2 * B * kDim * 4);
@@ -175,9 +186,12 @@ int ensure_ws(fac_ctx* c, int B) {
   }
   HIP_TRY(c, hipMemset(c->ws, 0, L.total));
   char* base = (char*)c->ws;
-  const size_t half = (L.stem - L.act) / 2;
+  const size_t half = (L.deep - L.act) / 2, dhalf = (L.stem - L.deep) / 2;
   c->act0 = (uint16_t*)(base + L.act);
   c->act1 = (uint16_t*)(base + L.act + half);
+  c->deep0 = (uint16_t*)(base + L.deep);
+  c->deep1 = (uint16_t*)(base + L.deep + dhalf);
+  c->cap_chunk = L.cb;
   c->stem_out = (uint16_t*)(base + L.stem);
   c->slab = (float*)(base + L.slab);
   c->x = (float*)(base + L.x);
@@ -353,11 +367,13 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
   return FAC_OK;
 }
 
-// Optional per-stage event timing (fac_profile_forward_u8) and early exit
-// after conv `stop_after` (fac_debug_features_u8, -1 = full forward).
+// Optional per-stage event timing (fac_profile_forward_u8): an event after
+// every stage, tagged with the stage id; durations are summed per stage over
+// stem chunks.  stop_after >= 0 (fac_debug_features_u8) copies conv
+// `stop_after`'s output to feat_out and returns.
 struct Prof {
-  hipEvent_t ev[24];
-  int n = 0;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> stage;
 };
 
 int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
@@ -373,46 +389,82 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   const int dt = c->dtype;
-  const int chunk = (c->stem_chunk > 0 && c->stem_chunk < B && !prof && stop_after < 0) ? c->stem_chunk : B;
-#define MARK()                                                       \
-  do {                                                               \
-    if (prof) HIP_TRY(c, hipEventRecord(prof->ev[prof->n++], st));  \
+  const int chunk = std::min(B, c->cap_chunk);
+#define MARK(sid)                                  \
+  do {                                             \
+    if (prof) {                                    \
+      hipEvent_t mk_;                              \
+      HIP_TRY(c, hipEventCreate(&mk_));            \
+      prof->ev.push_back(mk_);                     \
+      prof->stage.push_back(sid);                  \
+      HIP_TRY(c, hipEventRecord(mk_, st));         \
+    }                                              \
   } while (0)
-  MARK();
+  auto conv_out_elems = [](const ConvLayer& L) {  // per crop
+    const size_t Ho = L.pool ? L.H / 2 : L.H;
+    return Ho * Ho * (size_t)L.Cout;
+  };
+  MARK(-1);
+  // Stage A, per stem chunk (a sub-batch whose high-res activations can stay
+  // in the Infinity Cache): conv1..conv9, output pooled 28x28x128 into the
+  // whole-batch deep buffer.
   for (int b0 = 0; b0 < B && !stem_in; b0 += chunk) {
     const int nb = std::min(chunk, B - b0);
+    if (nb > c->cap_chunk) return set_err(c, FAC_ERR_ARG, "internal: stem chunk exceeds workspace");
     const void* src = u8 ? (const void*)((const uint8_t*)in + (size_t)b0 * kImg * kImg * 3)
                          : (const void*)((const float*)in + (size_t)b0 * 3 * kImg * kImg);
     uint16_t *cur = c->act0, *nxt = c->act1;
     int l0 = 0;
+    bool copied = false;  // stop_after's output already copied for this chunk
     if (c->fuse_stem224 && (stop_after < 0 || stop_after >= 2)) {
-      // conv1..conv3 + pool in one kernel; the profile reports it as stage conv1
+      // conv1..conv3 + pool in one kernel; the profile reports it as stage 0 (conv1)
       HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_w, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
                                 c->conv[1].b, cur, nb, c->num_cu, st));
-      MARK();
-      MARK();
-      MARK();
+      MARK(0);
       l0 = 2;
       if (stop_after == 2) {
-        HIP_TRY(c, hipMemcpyAsync(feat_out, cur, (size_t)nb * 112 * 112 * 32 * 2, hipMemcpyDeviceToDevice, st));
-        return FAC_OK;
+        HIP_TRY(c, hipMemcpyAsync(feat_out + (size_t)b0 * conv_out_elems(c->conv[1]), cur,
+                                  (size_t)nb * conv_out_elems(c->conv[1]) * 2, hipMemcpyDeviceToDevice, st));
+        copied = true;
       }
     } else {
-      HIP_TRY(c, launch_conv1(dt, u8, src, c->conv1_w, c->conv1_b, c->act0, nb, kImg, kImg, st));
-      MARK();
+      HIP_TRY(c, launch_conv1(dt, u8, src, c->conv1_w, c->conv1_b, cur, nb, kImg, kImg, st));
+      MARK(0);
       if (stop_after == 0) {
-        HIP_TRY(c, hipMemcpyAsync(feat_out, cur, (size_t)nb * kImg * kImg * 32 * 2, hipMemcpyDeviceToDevice, st));
-        return FAC_OK;
+        HIP_TRY(c, hipMemcpyAsync(feat_out + (size_t)b0 * kActElems, cur, (size_t)nb * kActElems * 2,
+                                  hipMemcpyDeviceToDevice, st));
+        copied = true;
       }
     }
-    for (int l = l0; l < 16; ++l) {
+    for (int l = l0; l <= kLastChunked && !copied; ++l) {
       const ConvLayer& L = c->conv[l];
-      uint16_t* dst = (l == 15) ? c->stem_out + (size_t)b0 * kPatchDim : nxt;
+      uint16_t* dst = (l == kLastChunked) ? c->deep0 + (size_t)b0 * conv_out_elems(L) : nxt;
       HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, nb, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st));
-      MARK();
+      MARK(l + 1);
+      if (stop_after == l + 1 && l != kLastChunked) {
+        HIP_TRY(c, hipMemcpyAsync(feat_out + (size_t)b0 * conv_out_elems(L), dst, (size_t)nb * conv_out_elems(L) * 2,
+                                  hipMemcpyDeviceToDevice, st));
+        copied = true;
+      }
+      std::swap(cur, nxt);
+    }
+  }
+  if (stop_after >= 0 && stop_after <= kLastChunked) return FAC_OK;  // copied per chunk above
+  // Stage B, whole batch: conv10..conv17 -> stem_out [B,7,7,512].
+  if (!stem_in) {
+    uint16_t *cur = c->deep0, *nxt = c->deep1;
+    if (stop_after == kLastChunked + 1) {
+      HIP_TRY(c, hipMemcpyAsync(feat_out, cur, (size_t)B * conv_out_elems(c->conv[kLastChunked]) * 2,
+                                hipMemcpyDeviceToDevice, st));
+      return FAC_OK;
+    }
+    for (int l = kLastChunked + 1; l < 16; ++l) {
+      const ConvLayer& L = c->conv[l];
+      uint16_t* dst = (l == 15) ? c->stem_out : nxt;
+      HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st));
+      MARK(l + 1);
       if (stop_after == l + 1) {
-        const int Ho = L.pool ? L.H / 2 : L.H;
-        HIP_TRY(c, hipMemcpyAsync(feat_out, dst, (size_t)nb * Ho * Ho * L.Cout * 2, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(c, hipMemcpyAsync(feat_out, dst, (size_t)B * conv_out_elems(L) * 2, hipMemcpyDeviceToDevice, st));
         return FAC_OK;
       }
       std::swap(cur, nxt);
@@ -422,7 +474,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, stem_in ? stem_in : c->stem_out, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
                          kPatchDim, S, st));
   HIP_TRY(c, launch_embed_finalize(c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->errflag, st));
-  MARK();
+  MARK(17);
   const int R = 2 * B;
   const float scale = 1.0f / std::sqrt((float)kDim);  // dim ** -0.5 (cvit.py:38), not head_dim
   // The two N=1024 projections (to_out, FF2) run split-K into fp32 partial
@@ -443,11 +495,11 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st));
     HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->hbuf, kMlp, T.w2, kMlp, nullptr, c->slab, kDim, R, kDim, kMlp, SK, st));
   }
-  MARK();
+  MARK(18);
   HIP_TRY(c, launch_resid_cls(dt, c->x, c->slab, SK, c->tl[kDepth - 1].b2, c->cbuf, B, st));
   HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, c->hh, kMlp, B, kMlp, kDim, 1, st));
   HIP_TRY(c, launch_head_out(c->hh, c->h2_w, c->h2_b, logits, probs, B, st));
-  MARK();
+  MARK(19);
 #undef MARK
   return FAC_OK;
 }
@@ -551,13 +603,18 @@ int fac_profile_forward_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t
   if (!c || !stage_ms || n_stages < FAC_PROFILE_STAGES) return set_err(c, FAC_ERR_ARG, "bad profile arguments");
   DevGuard g(c->device);
   Prof p;
-  for (int i = 0; i <= FAC_PROFILE_STAGES; ++i) HIP_TRY(c, hipEventCreate(&p.ev[i]));
   int rc = forward_impl(c, d_in, true, B, d_pos, d_logits, nullptr, stream, &p);
-  if (rc == FAC_OK) {
-    HIP_TRY(c, hipEventSynchronize(p.ev[p.n - 1]));
-    for (int i = 0; i + 1 < p.n && i < FAC_PROFILE_STAGES; ++i) HIP_TRY(c, hipEventElapsedTime(&stage_ms[i], p.ev[i], p.ev[i + 1]));
+  for (int i = 0; i < FAC_PROFILE_STAGES; ++i) stage_ms[i] = 0.f;
+  if (rc == FAC_OK && !p.ev.empty()) {
+    HIP_TRY(c, hipEventSynchronize(p.ev.back()));
+    for (size_t i = 1; i < p.ev.size(); ++i) {
+      if (p.stage[i] < 0 || p.stage[i] >= FAC_PROFILE_STAGES) continue;
+      float ms = 0.f;
+      HIP_TRY(c, hipEventElapsedTime(&ms, p.ev[i - 1], p.ev[i]));
+      stage_ms[p.stage[i]] += ms;
+    }
   }
-  for (int i = 0; i <= FAC_PROFILE_STAGES; ++i) (void)hipEventDestroy(p.ev[i]);
+  for (hipEvent_t e : p.ev) (void)hipEventDestroy(e);
   return rc;
 }
 

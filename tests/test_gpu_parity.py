@@ -307,6 +307,29 @@ def test_graph_capture_replay_matches_eager(models):
     assert torch.equal(out, eager)
 
 
+def test_stem_chunking_is_bit_exact(models):
+    """Running conv1..conv9 in sub-batches (Infinity-Cache-sized stem chunks)
+    changes nothing: same kernels per crop, so logits and features are identical."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models["fp16"]
+    crops = make_crops(100, seed=18)
+    slots = np.arange(100) % 32
+    base = _run_u8(m, crops, slots)
+    x = torch.from_numpy(crops[:40]).to(DEV)
+    feats = {}
+    for chunk in (0, 48, 17):
+        _lib.check(lib.fac_set_option(m._ctx, b"stem_chunk", chunk), m._ctx, "opt")
+        if chunk:
+            assert np.array_equal(_run_u8(m, crops, slots), base), chunk
+        f = torch.empty(40, 56, 56, 64, dtype=torch.float16, device=DEV)
+        _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), 40, 5, f.data_ptr(), None), m._ctx, "dbg")
+        torch.cuda.synchronize()
+        feats[chunk] = f.cpu()
+    _lib.check(lib.fac_set_option(m._ctx, b"stem_chunk", 0), m._ctx, "opt")
+    assert torch.equal(feats[0], feats[48]) and torch.equal(feats[0], feats[17])
+
+
 def test_large_batch_properties(models):
     """B=512 (beyond the goldens): finite, and bit-identical to scoring the same crops as a B=64 batch."""
     m = models["fp16"]
