@@ -90,6 +90,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-fuse", action="store_true", help="unfused conv1..conv3 (A/B of the fused 224 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="fac_set_option knob (include/fac_cvit.h), repeatable")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 
@@ -114,6 +116,9 @@ def main():
     ctx = model._ctx
     if args.no_fuse:
         _lib.check(lib.fac_set_option(ctx, b"fuse_stem224", 0), ctx, "set_option")
+    for kv in args.opt:
+        k, v = kv.split("=")
+        model.set_option(k, int(v))
 
     crops = torch.from_numpy(make_crops(B, seed=3 + rank)).to(dev)      # synthetic, resident in HBM
     pidx = (torch.arange(B, device=dev) % 32).to(torch.int32)
@@ -213,7 +218,7 @@ def main():
                    "model": "CViT(224,7,2,512,1024,6,8,2048)", "global_batch": world * B, "seq_len": 2,
                    "parallelism": f"frame-sharded x{world}" + (" + RCCL logit all-gather" if world > 1 else ""),
                    "graph": graph is not None, "stem_chunk": args.stem_chunk,
-                   "fused_stem224": not args.no_fuse},
+                   "fused_stem224": not args.no_fuse, **({"options": args.opt} if args.opt else {})},
         "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
         "roofline": {"bound": "mfma", "kernel": dom_name,
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

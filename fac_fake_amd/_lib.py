@@ -37,6 +37,9 @@ SIGNATURES = {
                                       ctypes.c_void_p]),
     "fac_debug_tail": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p]),
+    "fac_debug_gemm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "fac_profile_forward_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
                                               ctypes.c_void_p]),

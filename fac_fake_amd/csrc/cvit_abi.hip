@@ -27,7 +27,7 @@ hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, co
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
                         int B, int H, int W, hipStream_t st);
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
-                       void* out, int ldo, int M, int N, int K, int splits, hipStream_t st);
+                       void* out, int ldo, int M, int N, int K, int splits, hipStream_t st, int variant = -1);
 hipError_t launch_embed_finalize(const float* slab, int S, int B, const float* bias, const float* cls,
                                  const float* pos, const int32_t* pidx, float* x, int* err, hipStream_t st);
 hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,
@@ -104,6 +104,10 @@ struct fac_ctx {
   int cap_B = 0;
   int stem_chunk = 0;
   int fuse_stem224 = 1;  // conv1..conv3+pool as one persistent kernel (stem224.hip)
+  // GEMM tile variant per call site (transformer.hip launch_gemm; -1 = default)
+  // and the split-K factor of the two N=1024 projections (to_out, FF2)
+  int gemm_var[6] = {-1, -1, -1, -1, -1, -1};  // patch, qkv, out, ff1, ff2, head
+  int proj_splits = 4;
   int num_cu = 256;
   uint16_t *act0 = nullptr, *act1 = nullptr, *deep0 = nullptr, *deep1 = nullptr, *stem_out = nullptr, *xn = nullptr,
            *o = nullptr, *hbuf = nullptr, *cbuf = nullptr;
@@ -132,7 +136,7 @@ uint16_t to16(int dtype, float f) { return dtype == 0 ? fac_host::f32_to_bf16(f)
 // Split-K factor of the patch embedding (K = 25088 = 392 k-tiles of 64).  Fixed,
 // so a crop's logits are bit-identical whatever batch it is scored in.
 constexpr int kPatchSplits = 14;
-constexpr int kProjSplits = 4;  // split-K of the to_out / FF2 projections
+constexpr int kProjSplitsMax = 4;  // split-K of the to_out / FF2 projections (fac_ctx::proj_splits)
 int patch_splits(int) { return kPatchSplits; }
 
 struct WsLayout {
@@ -152,7 +156,7 @@ WsLayout layout(int B, int chunk) {
   WsLayout L{};
   const int cb = (chunk > 0 && chunk < B) ? chunk : B;
   L.cb = cb;
-  const size_t S = (size_t)std::max(kPatchSplits, 2 * kProjSplits) * B;
+  const size_t S = (size_t)std::max(kPatchSplits, 2 * kProjSplitsMax) * B;
   size_t off = 0;
   L.act = off; off += 2 * al((size_t)cb * kActElems * 2);
   L.deep = off; off += 2 * al((size_t)B * kDeepElems * 2);
@@ -472,7 +476,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   }
   const int S = patch_splits(B);
   HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, stem_in ? stem_in : c->stem_out, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
-                         kPatchDim, S, st));
+                         kPatchDim, S, st, c->gemm_var[0]));
   HIP_TRY(c, launch_embed_finalize(c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->errflag, st));
   MARK(17);
   const int R = 2 * B;
@@ -480,7 +484,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   // The two N=1024 projections (to_out, FF2) run split-K into fp32 partial
   // slabs; the following kernel (residual add + next LayerNorm, or the CLS
   // finish after the last layer) sums them in split order.
-  constexpr int SK = kProjSplits;
+  const int SK = c->proj_splits;
   for (int l = 0; l < kDepth; ++l) {
     const TLayer& T = c->tl[l];
     if (l == 0) {
@@ -488,16 +492,19 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     } else {
       HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, c->tl[l - 1].b2, T.ln1_g, T.ln1_b, c->xn, R, st));
     }
-    HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st,
+                           c->gemm_var[1]));
     HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
-    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st, c->gemm_var[2]));
     HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, T.bo, T.ln2_g, T.ln2_b, c->xn, R, st));
-    HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st));
-    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->hbuf, kMlp, T.w2, kMlp, nullptr, c->slab, kDim, R, kDim, kMlp, SK, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st,
+                           c->gemm_var[3]));
+    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->hbuf, kMlp, T.w2, kMlp, nullptr, c->slab, kDim, R, kDim, kMlp, SK, st, c->gemm_var[4]));
   }
   MARK(18);
   HIP_TRY(c, launch_resid_cls(dt, c->x, c->slab, SK, c->tl[kDepth - 1].b2, c->cbuf, B, st));
-  HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, c->hh, kMlp, B, kMlp, kDim, 1, st));
+  HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, c->hh, kMlp, B, kMlp, kDim, 1, st,
+                         c->gemm_var[5]));
   HIP_TRY(c, launch_head_out(c->hh, c->h2_w, c->h2_b, logits, probs, B, st));
   MARK(19);
 #undef MARK
@@ -565,6 +572,18 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     c->fuse_stem224 = value != 0;
     return FAC_OK;
   }
+  static const char* gemm_keys[6] = {"gemm_patch", "gemm_qkv", "gemm_out", "gemm_ff1", "gemm_ff2", "gemm_head"};
+  for (int i = 0; i < 6; ++i)
+    if (k == gemm_keys[i]) {
+      if (value < -1 || value > 3) return set_err(c, FAC_ERR_ARG, "gemm variant must be -1..3");
+      c->gemm_var[i] = value;
+      return FAC_OK;
+    }
+  if (k == "proj_splits") {
+    if (value != 1 && value != 2 && value != 4) return set_err(c, FAC_ERR_ARG, "proj_splits must be 1, 2 or 4");
+    c->proj_splits = value;
+    return FAC_OK;
+  }
   return set_err(c, FAC_ERR_ARG, "unknown option " + k);
 }
 
@@ -576,6 +595,16 @@ int fac_forward_nchw_f32(fac_ctx* c, const float* d_in, int B, const int32_t* d_
 int fac_forward_nhwc_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,
                         void* stream) {
   return forward_impl(c, d_in, true, B, d_pos, d_logits, d_probs, stream);
+}
+
+int fac_debug_gemm(fac_ctx* c, int epi, const uint16_t* d_a, const uint16_t* d_w, const float* d_bias, void* d_out,
+                   int M, int N, int K, int splits, int variant, void* stream) {
+  if (!c || !d_a || !d_w || !d_out) return set_err(c, FAC_ERR_ARG, "bad debug_gemm arguments");
+  const hipError_t e = fac::launch_gemm(c->dtype, epi, d_a, K, d_w, K, d_bias, d_out, N, M, N, K, splits,
+                                   (hipStream_t)stream, variant);
+  if (e != hipSuccess) return set_err(c, e == hipErrorInvalidValue ? FAC_ERR_ARG : FAC_ERR_HIP,
+                                      std::string("debug_gemm: ") + hipGetErrorString(e));
+  return FAC_OK;
 }
 
 int fac_debug_features_u8(fac_ctx* c, const uint8_t* d_in, int B, int layer, uint16_t* d_out, void* stream) {

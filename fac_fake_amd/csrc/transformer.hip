@@ -19,104 +19,109 @@ enum GemmEpi : int {
   EPI_T = 5,          // out T = acc + bias
 };
 
-// 64x64 output tile, BK = 64, 4 waves in a 2x2 grid (32x32 each = 2x2 MFMA
-// 16x16x32 tiles).  K-tiles stream through a 3-slot LDS ring: tile s is
-// fetched into register set s & 1 at the top of step s-2 and written to slot
-// s % 3 at the end of step s-1, so every fetch has two steps of MFMA work to
-// land (the per-step L2 latency was what bound these small-M GEMMs).
-// blockIdx.z selects a K range of Kper (split-K; Kper / 64 must be even).
-template <class T, int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt(const uint16_t* __restrict__ A, int lda,
-                                                  const uint16_t* __restrict__ Wt, int ldw,
-                                                  const float* __restrict__ bias, void* __restrict__ out_,
-                                                  int ldo, int M, int N, int Kper) {
-  constexpr int BM = 64, BN = 64, BK = 64, PS = BK + 8;
-  constexpr int SLOT = (BM + BN) * PS;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[3 * SLOT];
+// Async global -> LDS copy of 16 bytes per lane (global_load_lds_dwordx4).
+__device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
+}
+
+// C[M][N] = A[M][K] . W[N][K]^T on a BM x 128 output tile (BM = 32 or 64),
+// BK = 64, 4 waves in a WM x (4/WM) grid, each wave FM x FN MFMA 16x16x32
+// tiles.  Both operand tiles go global -> LDS by global_load_lds into an
+// NS-slot ring: tile kt lives in slot kt % NS and is issued NS-1 steps ahead
+// (GPW glds per wave per tile, counted in vmcnt; wait + barrier in one asm
+// statement so no LDS access can sit between them).  These GEMMs have
+// M = 2B = 512 rows and K = 1024..2048: they are latency-bound, and the ring
+// depth is what hides the HBM/L2 latency.  LDS rows are 128 B (64 k); the
+// 16-byte chunk c of row r sits at position c ^ ((r >> 1) & 7), applied on
+// the glds SOURCE address (the LDS side of a glds is lane-linear) and on the
+// fragment read: conflict-free for the ds_read_b128 lane groups.
+// blockIdx.z selects a K range of Kper (split-K; Kper % 64 == 0).
+template <class T, int EPI, int BM, int WM, int NS>
+__global__ __launch_bounds__(256, NS <= 3 ? 2 : 1) void gemm_nt(const uint16_t* __restrict__ A, int lda,
+                                                                const uint16_t* __restrict__ Wt, int ldw,
+                                                                const float* __restrict__ bias,
+                                                                void* __restrict__ out_, int ldo, int M, int N,
+                                                                int Kper) {
+  constexpr int BN = 128, BK = 64, WN = 4 / WM;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int SLOT = (BM + BN) * BK;    // elements
+  constexpr int GPW = (BM + BN) / 8 / 4;  // glds per wave per tile (8 rows per instruction)
+  static_assert((BM + BN) % 32 == 0 && FM >= 1 && FN >= 1 && NS >= 3, "gemm tile");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NS * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int k0 = blockIdx.z * Kper;
   const int nkt = Kper / BK;
 
-  // per-thread staging coordinates: rows r0, r0+32 of both tiles, 16-byte piece q
-  const int r0 = tid >> 3, q = tid & 7;
-  const bool va0 = m0 + r0 < M, va1 = m0 + r0 + 32 < M;
-  const uint16_t* pa0 = A + (size_t)(va0 ? m0 + r0 : 0) * lda + k0 + q * 8;
-  const uint16_t* pa1 = A + (size_t)(va1 ? m0 + r0 + 32 : 0) * lda + k0 + q * 8;
-  const uint16_t* pb0 = Wt + (size_t)(n0 + r0) * ldw + k0 + q * 8;
-  const uint16_t* pb1 = Wt + (size_t)(n0 + r0 + 32) * ldw + k0 + q * 8;
-  const int so0 = r0 * PS + q * 8, so1 = (r0 + 32) * PS + q * 8;
-
-  u16x8 rg[2][4];
-  auto load = [&](u16x8* r, int kt) {
-    const int ko = kt * BK;
-    r[0] = va0 ? *(const u16x8*)(pa0 + ko) : (u16x8)0;
-    r[1] = va1 ? *(const u16x8*)(pa1 + ko) : (u16x8)0;
-    r[2] = *(const u16x8*)(pb0 + ko);
-    r[3] = *(const u16x8*)(pb1 + ko);
-  };
-  auto store = [&](const u16x8* r, int slot) {
-    uint16_t* sa = smem + slot * SLOT;
-    uint16_t* sb = sa + BM * PS;
-    *(u16x8*)(sa + so0) = r[0];
-    *(u16x8*)(sa + so1) = r[1];
-    *(u16x8*)(sb + so0) = r[2];
-    *(u16x8*)(sb + so1) = r[3];
-  };
-
-  f32x4 acc[2][2];
+  // this lane's glds sources: instruction i of this wave covers tile rows
+  // 8*(4i + wave) .. +7 (rows < BM: A, else W), lane -> (row, position)
+  const uint16_t* gsrc[GPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = (f32x4)0.f;
+  for (int i = 0; i < GPW; ++i) {
+    const int row = 8 * (4 * i + wave) + (lane >> 3), pos = lane & 7;
+    const int c = pos ^ ((row >> 1) & 7);
+    if (row < BM) {
+      const int m = m0 + row < M ? m0 + row : M - 1;  // rows past M: any valid row, never stored
+      gsrc[i] = A + (size_t)m * lda + k0 + c * 8;
+    } else {
+      gsrc[i] = Wt + (size_t)(n0 + row - BM) * ldw + k0 + c * 8;
+    }
+  }
+  // tiles past the end are dummy re-reads of tile 0 into slots never read again
+  auto issue = [&](int kt) {
+    const int slot = kt % NS, t = kt < nkt ? kt : 0;
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) glds16(gsrc[i] + t * BK, smem + slot * SLOT + 8 * (4 * i + wave) * BK);
+  };
 
-  auto compute = [&](int slot) {
-    const uint16_t* sa = smem + slot * SLOT;
-    const uint16_t* sb = sa + BM * PS;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4)0.f;
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) issue(t);
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NS - 2) * GPW) : "memory");
+  for (int kt = 0; kt < nkt; ++kt) {
+    issue(kt + NS - 1);  // into the slot consumed at kt-1 (all waves passed its barrier)
+    const uint16_t* sa = smem + (kt % NS) * SLOT;
+    const uint16_t* sb = sa + BM * BK;
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
-      u16x8 af[2], bfr[2];
+      const int c = ks * 4 + (lane >> 4);
+      u16x8 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        af[i] = *(const u16x8*)(sa + (wm * 32 + i * 16 + (lane & 15)) * PS + ks * 32 + (lane >> 4) * 8);
-        bfr[i] = *(const u16x8*)(sb + (wn * 32 + i * 16 + (lane & 15)) * PS + ks * 32 + (lane >> 4) * 8);
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * (BM / WM) + i * 16 + (lane & 15);
+        af[i] = *(const u16x8*)(sa + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * (BN / WN) + j * 16 + (lane & 15);
+        bfr[j] = *(const u16x8*)(sb + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+      }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
     }
-  };
-
-  load(rg[0], 0);
-  if (nkt > 1) load(rg[1], 1);
-  store(rg[0], 0);
-  __syncthreads();
-  int slot = 0;
-  for (int kt = 0; kt < nkt; kt += 2) {
-    // step kt (register set 0 free: its tile was stored at the end of step kt-1)
-    if (kt + 2 < nkt) load(rg[0], kt + 2);
-    compute(slot);
-    slot = slot == 2 ? 0 : slot + 1;
-    if (kt + 1 < nkt) store(rg[1], slot);
-    __syncthreads();
-    if (kt + 1 >= nkt) break;
-    // step kt+1 (register set 1 free)
-    if (kt + 3 < nkt) load(rg[1], kt + 3);
-    compute(slot);
-    slot = slot == 2 ? 0 : slot + 1;
-    if (kt + 2 < nkt) store(rg[0], slot);
-    __syncthreads();
+    // retire tile kt+1 (tiles kt+2 .. kt+NS-1 stay in flight)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((NS - 2) * GPW) : "memory");
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tiles
 
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 32 + j * 16 + (lane & 15);
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
     const float bv = (EPI == EPI_PARTIAL || bias == nullptr) ? 0.f : bias[n];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
         if (m >= M) continue;
         const float v = acc[i][j][r] + bv;
         if constexpr (EPI == EPI_F32) {
@@ -386,27 +391,49 @@ __global__ __launch_bounds__(1024) void video_score(const float* __restrict__ lo
 
 namespace fac {
 
+// Tile variants (BM, WM, NS): 0 = 64x128 ring 3 (2 WG/CU), 1 = 64x128 ring 6,
+// 2 = 32x128 ring 3 (2 WG/CU), 3 = 32x128 ring 7.
+template <class T, int EPI>
+static void launch_gemm_v(int variant, dim3 grid, const uint16_t* A, int lda, const uint16_t* W, int ldw,
+                          const float* bias, void* out, int ldo, int M, int N, int Kper, hipStream_t st) {
+  switch (variant) {
+    case 0: gemm_nt<T, EPI, 64, 2, 3><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case 1: gemm_nt<T, EPI, 64, 2, 6><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case 2: gemm_nt<T, EPI, 32, 1, 3><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    default: gemm_nt<T, EPI, 32, 1, 7><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+  }
+}
+
 template <class T>
 static hipError_t launch_gemm_t(int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
-                                void* out, int ldo, int M, int N, int K, int splits, hipStream_t st) {
-  dim3 grid(N / 64, (M + 63) / 64, splits);
+                                void* out, int ldo, int M, int N, int K, int splits, int variant, hipStream_t st) {
+  const int bm = variant >= 2 ? 32 : 64;
+  dim3 grid(N / 128, (M + bm - 1) / bm, splits);
   const int Kper = K / splits;
   switch (epi) {
-    case EPI_F32: gemm_nt<T, EPI_F32><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
-    case EPI_F32_RELU: gemm_nt<T, EPI_F32_RELU><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
-    case EPI_T_GELU: gemm_nt<T, EPI_T_GELU><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
-    case EPI_RESID: gemm_nt<T, EPI_RESID><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
-    case EPI_PARTIAL: gemm_nt<T, EPI_PARTIAL><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
-    default: gemm_nt<T, EPI_T><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case EPI_F32: launch_gemm_v<T, EPI_F32>(variant, grid, A, lda, W, ldw, bias, out, ldo, M, N, Kper, st); break;
+    case EPI_F32_RELU: launch_gemm_v<T, EPI_F32_RELU>(variant, grid, A, lda, W, ldw, bias, out, ldo, M, N, Kper, st); break;
+    case EPI_T_GELU: launch_gemm_v<T, EPI_T_GELU>(variant, grid, A, lda, W, ldw, bias, out, ldo, M, N, Kper, st); break;
+    case EPI_RESID: launch_gemm_v<T, EPI_RESID>(variant, grid, A, lda, W, ldw, bias, out, ldo, M, N, Kper, st); break;
+    case EPI_PARTIAL: launch_gemm_v<T, EPI_PARTIAL>(variant, grid, A, lda, W, ldw, bias, out, ldo, M, N, Kper, st); break;
+    default: launch_gemm_v<T, EPI_T>(variant, grid, A, lda, W, ldw, bias, out, ldo, M, N, Kper, st); break;
   }
   return hipGetLastError();
 }
 
+// variant < 0: pick by shape.  Measured on MI355X (tools/gemm_sweep.py, bf16,
+// B = 256): the 32x128 / ring-3 tile (2 WG/CU) wins every encoder GEMM
+// (M = 512, K = 1024..2048: QKV 11.1 us, FF1 11.5, FF2/4 7.1, head 8.7 vs
+// 13-18 us for 64x128); deeper rings at 1 WG/CU lose.  The long-K patch
+// GEMM (K = 25088, split 14) prefers 64x128 / ring 3 (28.5 us).
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
-                       void* out, int ldo, int M, int N, int K, int splits, hipStream_t st) {
-  if (N % 64 != 0 || K % (128 * splits) != 0) return hipErrorInvalidValue;  // Kper: even number of 64-wide tiles
-  if (dtype == 0) return launch_gemm_t<BF16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, st);
-  return launch_gemm_t<F16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, st);
+                       void* out, int ldo, int M, int N, int K, int splits, hipStream_t st, int variant) {
+  if (N % 128 != 0 || splits < 1 || K % (64 * splits) != 0 || M <= 0 || epi < 0 || epi > EPI_T)
+    return hipErrorInvalidValue;
+  if (variant < 0) variant = K / splits >= 1024 && K >= 8192 ? 0 : 2;
+  if (variant > 3) return hipErrorInvalidValue;
+  if (dtype == 0) return launch_gemm_t<BF16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, variant, st);
+  return launch_gemm_t<F16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, variant, st);
 }
 
 hipError_t launch_embed_finalize(const float* slab, int S, int B, const float* bias, const float* cls,

@@ -144,6 +144,24 @@ class CViT(nn.Module):
             raise RuntimeError("no device context yet: call reserve() or forward() first")
         _lib.check(_lib.load().fac_set_stem_chunk(self._ctx, int(crops)), self._ctx, "fac_set_stem_chunk")
 
+    def set_option(self, key: str, value: int):
+        """fac_set_option knobs (include/fac_cvit.h): stem_chunk, fuse_stem224,
+        gemm_{patch,qkv,out,ff1,ff2,head}, proj_splits."""
+        if self._ctx is None:
+            raise RuntimeError("no device context yet: call reserve() or forward() first")
+        _lib.check(_lib.load().fac_set_option(self._ctx, key.encode(), int(value)), self._ctx, "fac_set_option")
+
+    def debug_gemm(self, epi: int, a: torch.Tensor, w: torch.Tensor, bias, out: torch.Tensor, splits: int = 1,
+                   variant: int = -1):
+        """One encoder GEMM out = a . w^T through fac_debug_gemm (16-bit a [M,K], w [N,K])."""
+        M, K = a.shape
+        N = w.shape[0]
+        lib = self._ensure_ctx(a.device)
+        stream = torch.cuda.current_stream(a.device).cuda_stream
+        _lib.check(lib.fac_debug_gemm(self._ctx, int(epi), a.data_ptr(), w.data_ptr(),
+                                      bias.data_ptr() if bias is not None else None, out.data_ptr(),
+                                      M, N, K, int(splits), int(variant), stream), self._ctx, "fac_debug_gemm")
+
     def _release(self):
         if self._ctx is not None:
             _lib.load().fac_destroy(self._ctx)

@@ -94,12 +94,19 @@ int fac_forward_nhwc_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t*
  * its whole time is stage conv1 and conv2/conv3 read 0.
  * fac_debug_conv: run stem conv `layer` (1..16 = conv2..conv17) alone on a
  * given NHWC 16-bit input.  fac_debug_tail: patch embedding + transformer +
- * head from a given NHWC 16-bit stem output [B,7,7,512]. */
+ * head from a given NHWC 16-bit stem output [B,7,7,512].
+ * fac_debug_gemm: one encoder GEMM out[M][N] = A[M][K] . W[N][K]^T (16-bit
+ * row-major operands, fp32 accumulation) with epilogue `epi` (0 fp32 + bias,
+ * 1 fp32 relu, 2 16-bit gelu, 3 fp32 residual +=, 4 split-K fp32 partial
+ * slabs [splits][M][N], 5 16-bit + bias), tile `variant` (-1 default, 0..3):
+ * the nn.Linear calls of cvit.py:28,39,50,164 in isolation. */
 #define FAC_PROFILE_STAGES 20
 int fac_debug_features_u8(fac_ctx* ctx, const uint8_t* d_in, int B, int layer, uint16_t* d_out, void* stream);
 int fac_debug_conv(fac_ctx* ctx, int layer, const uint16_t* d_in, int B, uint16_t* d_out, void* stream);
 int fac_debug_tail(fac_ctx* ctx, const uint16_t* d_stem, int B, const int32_t* d_pos_index, float* d_logits,
                    void* stream);
+int fac_debug_gemm(fac_ctx* ctx, int epi, const uint16_t* d_a, const uint16_t* d_w, const float* d_bias, void* d_out,
+                   int M, int N, int K, int splits, int variant, void* stream);
 int fac_profile_forward_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
                            float* stage_ms, int n_stages, void* stream);
 
@@ -116,7 +123,10 @@ int fac_video_score(const float* d_logits, int n, float* d_score, void* stream);
 int fac_set_stem_chunk(fac_ctx* ctx, int crops);
 
 /* Named knobs: "stem_chunk" (as above), "fuse_stem224" (1 = conv1..conv3 +
- * pool as one fused kernel, the default; 0 = one kernel per conv). */
+ * pool as one fused kernel, the default; 0 = one kernel per conv),
+ * "gemm_patch" / "gemm_qkv" / "gemm_out" / "gemm_ff1" / "gemm_ff2" /
+ * "gemm_head" (GEMM tile variant -1..3 per call site), "proj_splits" (split-K
+ * of to_out and FF2: 1, 2 or 4). */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);

@@ -339,3 +339,48 @@ def test_large_batch_properties(models):
     assert np.isfinite(big).all()
     small = _run_u8(m, crops[448:], slots[448:])
     assert np.array_equal(big[448:], small)     # a crop's logits do not depend on its batch
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_gemm_variants_vs_torch_fp32(models, dt, variant):
+    """Every GEMM tile variant and epilogue vs a torch fp32 matmul of the same
+    16-bit operands (fp32 accumulation: only the summation order differs, so
+    |err| <= 1e-5 * sum|a*w| per output).  M = 200 exercises the row clamp
+    (M not a multiple of the tile), K = 1024 / splits 4 the partial slabs."""
+    m = models[dt]
+    tdt = torch.float16 if dt == "fp16" else torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(7 + variant)
+    M, N, K = 200, 384, 1024
+    a = (torch.randn(M, K, generator=g) * 0.5).to(tdt).to(DEV)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(tdt).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    ref = a.float() @ w.float().t()
+    bound = 1e-5 * (a.float().abs() @ w.float().abs().t()) + 1e-6
+
+    def run(epi, out, splits=1):
+        m.debug_gemm(epi, a, w, bias, out, splits=splits, variant=variant)
+        torch.cuda.synchronize()
+        return out
+
+    o = run(0, torch.empty(M, N, device=DEV))
+    assert ((o - (ref + bias)).abs() <= bound).all()
+    o = run(1, torch.empty(M, N, device=DEV))
+    assert ((o - torch.relu(ref + bias)).abs() <= bound).all()
+    base = torch.randn(M, N, generator=g).to(DEV)
+    o = run(3, base.clone())
+    assert ((o - (base + ref + bias)).abs() <= bound + 1e-6 * base.abs()).all()
+    slabs = run(4, torch.empty(4, M, N, device=DEV), splits=4)
+    assert ((slabs.sum(0) - ref).abs() <= bound).all()
+    ref4 = torch.stack([a[:, i * 256:(i + 1) * 256].float() @ w[:, i * 256:(i + 1) * 256].float().t()
+                        for i in range(4)])
+    assert ((slabs - ref4).abs() <= bound).all()
+    # 16-bit outputs: within one rounding of the fp32 result
+    o = run(5, torch.empty(M, N, dtype=tdt, device=DEV)).float()
+    r = (ref + bias).to(tdt).float()
+    ulp = torch.finfo(tdt).eps * r.abs().clamp_min(torch.finfo(tdt).tiny)
+    assert ((o - r).abs() <= ulp + bound).all()
+    o = run(2, torch.empty(M, N, dtype=tdt, device=DEV)).float()
+    r = torch.nn.functional.gelu(ref + bias).to(tdt).float()
+    ulp = torch.finfo(tdt).eps * r.abs().clamp_min(1e-3)
+    assert ((o - r).abs() <= ulp + 2 * bound).all()
