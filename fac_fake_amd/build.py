@@ -35,6 +35,10 @@ def _flags():
             f"-I{CSRC}", f"-I{INCLUDE}"]
 
 
+# Per-file extra flags (none needed at present).
+FILE_FLAGS: dict = {}
+
+
 def _headers_mtime() -> float:
     hs = list(CSRC.glob("*.hpp")) + list(INCLUDE.glob("*.h"))
     return max((h.stat().st_mtime for h in hs), default=0.0)
@@ -54,7 +58,7 @@ def build(verbose: bool = False, force: bool = False) -> Path:
 
     def _compile(so):
         s, o = so
-        cmd = [hipcc, *_flags(), "-c", str(s), "-o", str(o)]
+        cmd = [hipcc, *_flags(), *FILE_FLAGS.get(s.name, []), "-c", str(s), "-o", str(o)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -139,6 +139,11 @@ constexpr int kPatchSplits = 14;
 constexpr int kProjSplitsMax = 4;  // split-K of the to_out / FF2 projections (fac_ctx::proj_splits)
 int patch_splits(int) { return kPatchSplits; }
 
+hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, uint16_t* out, int B, hipStream_t st) {
+  using namespace fac;
+  return launch_conv3x3(c->dtype, in, L.w, L.b, out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st);
+}
+
 struct WsLayout {
   size_t act, deep, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
   int cb;  // crops the high-res activation buffers hold (stem chunk)
@@ -443,7 +448,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     for (int l = l0; l <= kLastChunked && !copied; ++l) {
       const ConvLayer& L = c->conv[l];
       uint16_t* dst = (l == kLastChunked) ? c->deep0 + (size_t)b0 * conv_out_elems(L) : nxt;
-      HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, nb, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st));
+      HIP_TRY(c, run_conv(c, L, cur, dst, nb, st));
       MARK(l + 1);
       if (stop_after == l + 1 && l != kLastChunked) {
         HIP_TRY(c, hipMemcpyAsync(feat_out + (size_t)b0 * conv_out_elems(L), dst, (size_t)nb * conv_out_elems(L) * 2,
@@ -465,7 +470,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     for (int l = kLastChunked + 1; l < 16; ++l) {
       const ConvLayer& L = c->conv[l];
       uint16_t* dst = (l == 15) ? c->stem_out : nxt;
-      HIP_TRY(c, launch_conv3x3(dt, cur, L.w, L.b, dst, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st));
+      HIP_TRY(c, run_conv(c, L, cur, dst, B, st));
       MARK(l + 1);
       if (stop_after == l + 1) {
         HIP_TRY(c, hipMemcpyAsync(feat_out, dst, (size_t)B * conv_out_elems(L) * 2, hipMemcpyDeviceToDevice, st));
@@ -617,8 +622,7 @@ int fac_debug_conv(fac_ctx* c, int layer, const uint16_t* d_in, int B, uint16_t*
   if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "debug_conv before fac_load_weights");
   DevGuard g(c->device);
   const ConvLayer& L = c->conv[layer - 1];
-  HIP_TRY(c, fac::launch_conv3x3(c->dtype, d_in, L.w, L.b, d_out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16,
-                                 (hipStream_t)stream));
+  HIP_TRY(c, run_conv(c, L, d_in, d_out, B, (hipStream_t)stream));
   return FAC_OK;
 }
 
