@@ -8,14 +8,17 @@
 // uint8 pixels in and 0.8 MB of pooled 112x112x32 out.
 //
 // One persistent 512-thread workgroup per CU keeps all three weight tensors
-// in LDS (40 KB) and walks 16x16 output boxes.  Per box:
-//   A: normalised input over the 22x22 region (conv1's receptive field);
-//   B: conv1 over the 20x20 region conv2 needs -> LDS image c1;
-//   C: conv2 over the 18x18 region conv3 needs -> LDS image c2;
-//   D: conv3 over the 16x16 box, 2x2 max in registers -> 8x8x32 tile out.
+// in LDS (40 KB) and walks 16x32 output boxes.  Per box:
+//   A: normalised input over the 22x38 region (conv1's receptive field);
+//   B: conv1 over the 20x36 region conv2 needs -> LDS image c1;
+//   C: conv2 over the 18x34 region conv3 needs -> LDS image c2;
+//   D: conv3 over the 16x32 box, 2x2 max in registers -> 8x16x32 tile out.
 // Intermediate pixels that fall outside the image are stored as 0, which is
 // exactly the zero padding the next conv expects.  Recompute overhead:
-// conv1 x1.56, conv2 x1.27 (conv1 is 0.7% of the network's FLOPs).
+// conv1 x1.41, conv2 x1.20 (conv1 is 0.7% of the network's FLOPs).  The
+// 16x32 box (vs 16x16) cuts that recompute, gives every wave 4 conv3 row
+// tiles per weight fetch (conv3 LDS reads per MFMA 1.0 -> 0.75), balances
+// the row tiles over the 8 waves better and halves the barriers per pixel.
 //
 // conv1 and conv2 run "transposed" (C^T = W . X^T: MFMA rows = channels,
 // cols = pixels), so each lane ends with 4 consecutive channels of one pixel
@@ -47,9 +50,15 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
                                                         const uint16_t* __restrict__ w3g,
                                                         const float* __restrict__ b3,
                                                         uint16_t* __restrict__ out, int ntiles) {
-  constexpr int IMG = 224, TPR = 14, TPI = 196;   // 16x16 boxes per row / per image
-  constexpr int RP = 24;                          // LDS image row pitch (16-byte units, == 8 mod 16)
-  constexpr int P1 = 20 * RP + 8, P2 = 18 * RP + 8;  // plane pitches of c1 / c2 (simulated: 1.33-way / 1-way)
+  constexpr int IMG = 224, TPR = 7, TPI = 98;     // 16x32 boxes per box row / per image
+  constexpr int BW = 32;                          // box width (height 16)
+  constexpr int IW = BW + 6, IN_PIX = 22 * IW;    // input region 22 x 38
+  constexpr int C1W = BW + 4, C1_PIX = 20 * C1W;  // conv1 region 20 x 36 (45 row tiles)
+  constexpr int C2W = BW + 2, C2_PIX = 18 * C2W;  // conv2 region 18 x 34 (39 row tiles)
+  constexpr int RP = 40;                          // LDS image row pitch (16-byte units, == 8 mod 16)
+  // plane pitches of c1 / c2, by simulating the ds_read_b128 lane groups:
+  // conv2's reads of c1 1.18-way, conv3's reads of c2 conflict-free
+  constexpr int P1 = 20 * RP + 8, P2 = 18 * RP;
   constexpr int W1P = 72;                         // conv1 weight row pitch (elements)
   constexpr int WSZ = 9 * 4 * 32 * 8;             // conv2/3 weights: [tap][q][32][8]
   constexpr int OFF_W2 = 32 * W1P, OFF_W3 = OFF_W2 + WSZ, OFF_C1 = OFF_W3 + WSZ;
@@ -63,8 +72,8 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   uint16_t* const c1 = smem + OFF_C1;
   uint16_t* const c2 = smem + OFF_C2;
   uint16_t* const lut = smem + OFF_LUT;
-  uint16_t* const sin = c2;    // 22x22x4 input image: dead before conv2 writes c2
-  uint16_t* const ostg = c1;   // 64 x (32+8) pooled tile: c1 is dead after conv2
+  uint16_t* const sin = c2;    // 22x38x4 input image: dead before conv2 writes c2
+  uint16_t* const ostg = c1;   // 128 x (32+8) pooled tile: c1 is dead after conv2
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
@@ -96,61 +105,68 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     bn3[ct] = (f32x4)b3[ct * 16 + r16];
   }
   // Tile-invariant LDS offsets of this lane's rows in each stage.
-  int in_off[4][2], c1_wr[4];
+  constexpr int RT1 = (C1_PIX + 15) / 16, RT2 = (C2_PIX + 15) / 16;  // 45, 39
+  constexpr int N1 = (RT1 + 7) / 8, N2 = (RT2 + 7) / 8;              // 6, 5 row tiles per wave (max)
+  int in_off[N1][2], c1_wr[N1];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {  // conv1: row tiles wave + 8i (< 25), raster over 20x20
+  for (int i = 0; i < N1; ++i) {  // conv1: row tiles wave + 8i (< 45), raster over 20x36
     const int rt = wave + 8 * i;
-    const int m = (rt < 25 ? rt : 0) * 16 + r16;
-    const int cy = m / 20, cx = m - (m / 20) * 20;
+    const int m = (rt < RT1 ? rt : 0) * 16 + r16;
+    const int cy = m / C1W, cx = m - (m / C1W) * C1W;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int t = ks * 8 + 2 * g;  // taps t, t+1 (t+1 <= 9 only when t < 8)
-      in_off[i][ks] = ((cy + t / 3) * 22 + cx + t % 3) * 4;
+      in_off[i][ks] = ((cy + t / 3) * IW + cx + t % 3) * 4;
     }
     c1_wr[i] = ((g >> 1) * P1 + cy * RP + cx) * 8 + (g & 1) * 4;  // + ct*2*P1*8 (channels 16ct+4g..)
   }
-  int c2_rd[3], c2_wr[3];
+  int c2_rd[N2], c2_wr[N2];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {  // conv2: row tiles wave + 8i (< 21), window-major over 18x18
+  for (int i = 0; i < N2; ++i) {  // conv2: row tiles wave + 8i (< 39), window-major over 18x34
     int m = (wave + 8 * i) * 16 + r16;
-    if (m >= 324) m = 0;
+    if (m >= C2_PIX) m = 0;
     int py, px;
-    win_pixel<18>(m, py, px);
+    win_pixel<C2W>(m, py, px);
     c2_rd[i] = (g * P1 + py * RP + px) * 8;
     c2_wr[i] = ((g >> 1) * P2 + py * RP + px) * 8 + (g & 1) * 4;
   }
-  int c3_rd[2];
+  int c3_rd[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {  // conv3: row tiles 2*wave + i, window-major over 16x16
+  for (int i = 0; i < 4; ++i) {  // conv3: row tiles 4*wave + i, window-major over 16x32
     int py, px;
-    win_pixel<16>((wave * 2 + i) * 16 + r16, py, px);
+    win_pixel<BW>((wave * 4 + i) * 16 + r16, py, px);
     c3_rd[i] = (g * P2 + py * RP + px) * 8;
   }
 
-  // Raw input pixels of a box's 22x22 receptive field, fetched one box ahead
-  // (during conv2/conv3 of the previous box) so phase A never waits on HBM.
-  float raw0 = 0.f, raw1 = 0.f, raw2 = 0.f;  // U8: the byte values; F32: normalised floats
-  bool raw_in = false;
+  // Raw input pixels of a box's 22x38 receptive field (pixel tid and
+  // tid+512 of it), fetched one box ahead (during conv2/conv3 of the previous
+  // box) so phase A never waits on HBM.
+  float raw[2][3];  // U8: the byte values; F32: normalised floats
+  bool raw_in[2];
   auto fetch = [&](int tile) {
-    raw0 = raw1 = raw2 = 0.f;
-    raw_in = false;
-    if (tid >= 484 || tile >= ntiles) return;
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
-    const int iy = tid / 22, ix = tid - (tid / 22) * 22;
-    const int y = ty * 16 - 3 + iy, x = tx * 16 - 3 + ix;
-    if (y < 0 || y >= IMG || x < 0 || x >= IMG) return;
-    raw_in = true;
-    if constexpr (U8) {
-      const uint8_t* src = (const uint8_t*)in_ + (((size_t)b * IMG + y) * IMG + x) * 3;
-      raw0 = (float)src[0];
-      raw1 = (float)src[1];
-      raw2 = (float)src[2];
-    } else {
-      const float* src = (const float*)in_ + (size_t)b * 3 * IMG * IMG + (size_t)y * IMG + x;
-      raw0 = src[0];
-      raw1 = src[IMG * IMG];
-      raw2 = src[2 * IMG * IMG];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      raw[k][0] = raw[k][1] = raw[k][2] = 0.f;
+      raw_in[k] = false;
+      const int p = tid + 512 * k;
+      if (p >= IN_PIX || tile >= ntiles) continue;
+      const int iy = p / IW, ix = p - (p / IW) * IW;
+      const int y = ty * 16 - 3 + iy, x = tx * BW - 3 + ix;
+      if (y < 0 || y >= IMG || x < 0 || x >= IMG) continue;
+      raw_in[k] = true;
+      if constexpr (U8) {
+        const uint8_t* src = (const uint8_t*)in_ + (((size_t)b * IMG + y) * IMG + x) * 3;
+        raw[k][0] = (float)src[0];
+        raw[k][1] = (float)src[1];
+        raw[k][2] = (float)src[2];
+      } else {
+        const float* src = (const float*)in_ + (size_t)b * 3 * IMG * IMG + (size_t)y * IMG + x;
+        raw[k][0] = src[0];
+        raw[k][1] = src[IMG * IMG];
+        raw[k][2] = src[2 * IMG * IMG];
+      }
     }
   };
   fetch(blockIdx.x);
@@ -158,41 +174,45 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
-    const int y0 = ty * 16, x0 = tx * 16;
+    const int y0 = ty * 16, x0 = tx * BW;
     __syncthreads();  // previous tile's readers of sin(=c2) and ostg(=c1) are done
 
-    // ---- A: normalised 16-bit input over (y0-3 .. y0+18) x (x0-3 .. x0+18);
+    // ---- A: normalised 16-bit input over (y0-3 .. y0+18) x (x0-3 .. x0+34);
     // out-of-image pixels were fetched as 0 (zero padding in normalised space)
-    if (tid < 484) {
-      u16x4 h;
-      if constexpr (U8) {
-        h[0] = raw_in ? lut[(int)raw0] : (uint16_t)0;
-        h[1] = raw_in ? lut[256 + (int)raw1] : (uint16_t)0;
-        h[2] = raw_in ? lut[512 + (int)raw2] : (uint16_t)0;
-      } else {
-        h[0] = T::from_f32(raw0);
-        h[1] = T::from_f32(raw1);
-        h[2] = T::from_f32(raw2);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int p = tid + 512 * k;
+      if (p < IN_PIX) {
+        u16x4 h;
+        if constexpr (U8) {
+          h[0] = raw_in[k] ? lut[(int)raw[k][0]] : (uint16_t)0;
+          h[1] = raw_in[k] ? lut[256 + (int)raw[k][1]] : (uint16_t)0;
+          h[2] = raw_in[k] ? lut[512 + (int)raw[k][2]] : (uint16_t)0;
+        } else {
+          h[0] = T::from_f32(raw[k][0]);
+          h[1] = T::from_f32(raw[k][1]);
+          h[2] = T::from_f32(raw[k][2]);
+        }
+        h[3] = 0;
+        *(u16x4*)(sin + p * 4) = h;
       }
-      h[3] = 0;
-      *(u16x4*)(sin + tid * 4) = h;
     }
     __syncthreads();
     // interior boxes (no receptive field pixel outside the image) skip the zeroing
-    const bool interior = ty > 0 && ty < TPR - 1 && tx > 0 && tx < TPR - 1;
+    const bool interior = ty > 0 && ty < IMG / 16 - 1 && tx > 0 && tx < TPR - 1;
 
-    // ---- B: conv1 over the 20x20 region at (y0-2, x0-2): 25 row tiles, raster order
+    // ---- B: conv1 over the 20x36 region at (y0-2, x0-2): 45 row tiles, raster order
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < N1; ++i) {
       const int rt = wave + 8 * i;
-      if (rt >= 25) break;
+      if (rt >= RT1) break;
       f32x4 acc[2] = {bt1[0], bt1[1]};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int t0 = ks * 8 + 2 * g;
         u16x4 lo = (u16x4)0, hi = (u16x4)0;
         if (t0 < 9) lo = *(const u16x4*)(sin + in_off[i][ks]);
-        if (t0 + 1 < 9) hi = *(const u16x4*)(sin + in_off[i][ks] + ((t0 + 1) % 3 == 0 ? 22 * 4 - 2 * 4 : 4));
+        if (t0 + 1 < 9) hi = *(const u16x4*)(sin + in_off[i][ks] + ((t0 + 1) % 3 == 0 ? IW * 4 - 2 * 4 : 4));
         const u16x8 p = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
@@ -203,7 +223,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       bool inside = true;
       if (!interior) {
         const int m = rt * 16 + r16;
-        const int cy = m / 20, cx = m - (m / 20) * 20;
+        const int cy = m / C1W, cx = m - (m / C1W) * C1W;
         inside = (unsigned)(y0 - 2 + cy) < (unsigned)IMG && (unsigned)(x0 - 2 + cx) < (unsigned)IMG;
       }
 #pragma unroll
@@ -219,15 +239,15 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
 
     fetch(tile + gridDim.x);  // next box's pixels land while conv2/conv3 run
 
-    // ---- C: conv2 over the 18x18 region at (y0-1, x0-1): window-major, 21 row tiles
+    // ---- C: conv2 over the 18x34 region at (y0-1, x0-1): window-major, 39 row tiles
     {
-      f32x4 acc[3][2];
+      f32x4 acc[N2][2];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
+      for (int i = 0; i < N2; ++i) {
         acc[i][0] = bt2[0];
         acc[i][1] = bt2[1];
       }
-      const bool has3 = wave + 16 < 21;  // waves 0-4 own three row tiles, 5-7 two
+      const bool hasN = wave + 8 * (N2 - 1) < RT2;  // waves 0-6 own five row tiles, wave 7 four
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int toff = ((t / 3) * RP + (t % 3)) * 8;
@@ -235,21 +255,21 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw2 + ((t * 4 + g) * 32 + ct * 16 + r16) * 8);
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          if (i == 2 && !has3) continue;
+        for (int i = 0; i < N2; ++i) {
+          if (i == N2 - 1 && !hasN) continue;
           const u16x8 a = *(const u16x8*)(c1 + c2_rd[i] + toff);
 #pragma unroll
           for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(wf[ct], a, acc[i][ct]);
         }
       }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        if (i == 2 && !has3) continue;
+      for (int i = 0; i < N2; ++i) {
+        if (i == N2 - 1 && !hasN) continue;
         const int m = (wave + 8 * i) * 16 + r16;
-        bool keep = m < 324;
+        bool keep = m < C2_PIX;
         if (!interior && keep) {
           int py, px;
-          win_pixel<18>(m, py, px);
+          win_pixel<C2W>(m, py, px);
           keep = (unsigned)(y0 - 1 + py) < (unsigned)IMG && (unsigned)(x0 - 1 + px) < (unsigned)IMG;
         }
 #pragma unroll
@@ -258,17 +278,17 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] = T::from_f32(fmaxf(acc[i][ct][j], 0.f));
           if (!keep) o = (u16x4)0;
-          if (m < 324) *(u16x4*)(c2 + c2_wr[i] + ct * 2 * P2 * 8) = o;
+          if (m < C2_PIX) *(u16x4*)(c2 + c2_wr[i] + ct * 2 * P2 * 8) = o;
         }
       }
     }
     __syncthreads();
 
-    // ---- D: conv3 over the 16x16 box, window-major, 2x2 max-pool in registers
+    // ---- D: conv3 over the 16x32 box, window-major, 2x2 max-pool in registers
     {
-      f32x4 acc[2][2];
+      f32x4 acc[4][2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 4; ++i) {
         acc[i][0] = bn3[0];
         acc[i][1] = bn3[1];
       }
@@ -279,25 +299,25 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw3 + ((t * 4 + g) * 32 + ct * 16 + r16) * 8);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 4; ++i) {
           const u16x8 a = *(const u16x8*)(c2 + c3_rd[i] + toff);
 #pragma unroll
           for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(a, wf[ct], acc[i][ct]);
         }
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
           const f32x4 v = acc[i][ct];
           const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-          ostg[((wave * 2 + i) * 4 + g) * 40 + ct * 16 + r16] = T::from_f32(fmaxf(mx, 0.f));
+          ostg[((wave * 4 + i) * 4 + g) * 40 + ct * 16 + r16] = T::from_f32(fmaxf(mx, 0.f));
         }
     }
     __syncthreads();
-    if (tid < 256) {
+    {  // 128 pooled pixels x 4 16-byte channel quarters = 512 threads
       const int w = tid >> 2, q = tid & 3;
-      const int wy = w >> 3, wx = w & 7;
+      const int wy = w >> 4, wx = w & 15;
       *(u16x8*)(out + (((size_t)b * 112 + (y0 >> 1) + wy) * 112 + (x0 >> 1) + wx) * 32 + q * 8) =
           *(const u16x8*)(ostg + w * 40 + q * 8);
     }
@@ -307,7 +327,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
                           hipStream_t st) {
-  const int ntiles = B * 196;
+  const int ntiles = B * 98;  // 16x32 boxes
   const int grid = nwg < ntiles ? nwg : ntiles;
   if (dtype == 0) {
     if (u8) stem224_fused<BF16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
