@@ -28,8 +28,9 @@ hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, 
                         int B, int H, int W, hipStream_t st);
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
                        void* out, int ldo, int M, int N, int K, int splits, hipStream_t st, int variant = -1);
-hipError_t launch_embed_finalize(const float* slab, int S, int B, const float* bias, const float* cls,
-                                 const float* pos, const int32_t* pidx, float* x, int* err, hipStream_t st);
+hipError_t launch_embed_finalize_ln(int dtype, const float* slab, int S, int B, const float* bias, const float* cls,
+                                    const float* pos, const int32_t* pidx, float* x, const float* g, const float* bt,
+                                    uint16_t* y, int* err, hipStream_t st);
 hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,
                             hipStream_t st);
 hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipStream_t st);
@@ -482,7 +483,9 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   const int S = patch_splits(B);
   HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, stem_in ? stem_in : c->stem_out, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
                          kPatchDim, S, st, c->gemm_var[0]));
-  HIP_TRY(c, launch_embed_finalize(c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->errflag, st));
+  // residual stream rows + layer 0's PreNorm LayerNorm in one pass
+  HIP_TRY(c, launch_embed_finalize_ln(dt, c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->tl[0].ln1_g,
+                                      c->tl[0].ln1_b, c->xn, c->errflag, st));
   MARK(17);
   const int R = 2 * B;
   const float scale = 1.0f / std::sqrt((float)kDim);  // dim ** -0.5 (cvit.py:38), not head_dim
@@ -492,9 +495,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   const int SK = c->proj_splits;
   for (int l = 0; l < kDepth; ++l) {
     const TLayer& T = c->tl[l];
-    if (l == 0) {
-      HIP_TRY(c, launch_layernorm(dt, c->x, T.ln1_g, T.ln1_b, c->xn, R, st));
-    } else {
+    if (l > 0) {
       HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, c->tl[l - 1].b2, T.ln1_g, T.ln1_b, c->xn, R, st));
     }
     HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st,

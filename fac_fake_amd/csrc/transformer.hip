@@ -142,90 +142,14 @@ __global__ __launch_bounds__(256, NS <= 3 ? 2 : 1) void gemm_nt(const uint16_t* 
   }
 }
 
-// x[2b] = cls + pos[p_b];  x[2b+1] = (sum_s slab[s][b]) + bias + pos[p_b]
-// (cvit.py:171-175: patch_to_embedding, cat(cls, y), += pos_embedding[0:B],
-// with pos indexed by the crop's batch slot p_b).
-__global__ __launch_bounds__(256) void embed_finalize(const float* __restrict__ slab, int S, int B,
-                                                      const float* __restrict__ bias,
-                                                      const float* __restrict__ cls,
-                                                      const float* __restrict__ pos,
-                                                      const int32_t* __restrict__ pidx, float* __restrict__ x,
-                                                      int* __restrict__ err) {
-  const int b = blockIdx.x;
-  int p = pidx[b];
-  if (p < 0 || p >= 32) {
-    if (threadIdx.x == 0) atomicOr(err, 1);
-    p = p < 0 ? 0 : 31;
-  }
-  for (int n = threadIdx.x; n < 1024; n += 256) {
-    float y = 0.f;
-    for (int s = 0; s < S; ++s) y += slab[((size_t)s * B + b) * 1024 + n];
-    const float pe = pos[p * 1024 + n];
-    x[(size_t)(2 * b) * 1024 + n] = cls[n] + pe;
-    x[(size_t)(2 * b + 1) * 1024 + n] = (y + bias[n]) + pe;
-  }
-}
-
-// LayerNorm(1024, eps 1e-5) (PreNorm, cvit.py:13-20): one wave per row,
-// fp32 statistics, 16-bit output feeding the next GEMM.
+// LayerNorm(1024, eps 1e-5) of one row held by one wave (16 floats per lane:
+// columns i*256 + 4*lane + j) -> 16-bit (PreNorm, cvit.py:13-20).
 template <class T>
-__global__ __launch_bounds__(256) void layernorm_rows(const float* __restrict__ x, const float* __restrict__ g,
-                                                      const float* __restrict__ bta, uint16_t* __restrict__ y,
-                                                      int R) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= R) return;
-  const float* xr = x + (size_t)row * 1024;
-  f32x4 v[4];
+__device__ __forceinline__ void ln_row_store(const f32x4 (&v)[4], const float* __restrict__ g,
+                                             const float* __restrict__ bta, uint16_t* __restrict__ yr, int lane) {
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[i] = *(const f32x4*)(xr + i * 256 + lane * 4);
-    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-  }
-  const float mean = wave_sum(s) * (1.0f / 1024.0f);
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float d = v[i][j] - mean;
-      q += d * d;
-    }
-  const float var = wave_sum(q) * (1.0f / 1024.0f);
-  const float rstd = 1.0f / sqrtf(var + 1e-5f);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = i * 256 + lane * 4;
-    u16x4 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = T::from_f32((v[i][j] - mean) * rstd * g[c + j] + bta[c + j]);
-    *(u16x4*)(y + (size_t)row * 1024 + c) = o;
-  }
-}
-
-// Residual add of a split-K projection + the next PreNorm LayerNorm, fused:
-//   x[r] += (sum_s slab[s][r]) + bias      (Residual, cvit.py:10-11)
-//   y[r]  = LayerNorm(x[r]) * g + b -> 16-bit (PreNorm, cvit.py:19-20)
-// The partial sums are added in split order: deterministic, no atomics.
-template <class T>
-__global__ __launch_bounds__(256) void resid_layernorm(float* __restrict__ x, const float* __restrict__ slab, int S,
-                                                       const float* __restrict__ bias, const float* __restrict__ g,
-                                                       const float* __restrict__ bta, uint16_t* __restrict__ y,
-                                                       int R) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= R) return;
-  float* xr = x + (size_t)row * 1024;
-  f32x4 v[4];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = i * 256 + lane * 4;
-    f32x4 p = *(const f32x4*)(slab + (size_t)row * 1024 + c);
-    for (int k = 1; k < S; ++k) p += *(const f32x4*)(slab + ((size_t)k * R + row) * 1024 + c);
-    v[i] = (p + *(const f32x4*)(bias + c)) + *(const f32x4*)(xr + c);
-    *(f32x4*)(xr + c) = v[i];
-    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-  }
+  for (int i = 0; i < 4; ++i) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   const float mean = wave_sum(s) * (1.0f / 1024.0f);
   float q = 0.f;
 #pragma unroll
@@ -239,24 +163,101 @@ __global__ __launch_bounds__(256) void resid_layernorm(float* __restrict__ x, co
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = i * 256 + lane * 4;
+    const f32x4 gg = *(const f32x4*)(g + c), bb = *(const f32x4*)(bta + c);
     u16x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = T::from_f32((v[i][j] - mean) * rstd * g[c + j] + bta[c + j]);
-    *(u16x4*)(y + (size_t)row * 1024 + c) = o;
+    for (int j = 0; j < 4; ++j) o[j] = T::from_f32((v[i][j] - mean) * rstd * gg[j] + bb[j]);
+    *(u16x4*)(yr + c) = o;
   }
+}
+
+// Sum of the S split-K partial slabs of row `row` (slab s at (s*R + row)),
+// columns i*256 + 4*lane .. +3, added in split order (deterministic).  S is
+// a template argument so all S loads of a column group are in flight at once.
+template <int S>
+__device__ __forceinline__ f32x4 slab_sum(const float* __restrict__ slab, size_t R, int row, int c) {
+  f32x4 p = *(const f32x4*)(slab + (size_t)row * 1024 + c);
+#pragma unroll
+  for (int k = 1; k < S; ++k) p += *(const f32x4*)(slab + ((size_t)k * R + row) * 1024 + c);
+  return p;
+}
+
+// Token rows of the residual stream + layer 0's PreNorm, one wave per row
+// (cvit.py:171-175 patch_to_embedding, cat(cls, y), += pos_embedding[0:B]
+// with pos indexed by the crop's batch slot p_b; then cvit.py:19-20):
+//   x[2b]   = cls + pos[p_b]
+//   x[2b+1] = (sum_s slab[s][b]) + bias + pos[p_b]
+//   y[r]    = LayerNorm_0(x[r]) -> 16-bit
+template <class T, int S>
+__global__ __launch_bounds__(64) void embed_finalize_ln(const float* __restrict__ slab, int B,
+                                                        const float* __restrict__ bias,
+                                                        const float* __restrict__ cls,
+                                                        const float* __restrict__ pos,
+                                                        const int32_t* __restrict__ pidx, float* __restrict__ x,
+                                                        const float* __restrict__ g, const float* __restrict__ bta,
+                                                        uint16_t* __restrict__ y, int* __restrict__ err) {
+  const int r = blockIdx.x, b = r >> 1, lane = threadIdx.x;
+  int p = pidx[b];
+  if (p < 0 || p >= 32) {
+    if (lane == 0 && (r & 1) == 0) atomicOr(err, 1);
+    p = p < 0 ? 0 : 31;
+  }
+  f32x4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = i * 256 + lane * 4;
+    const f32x4 pe = *(const f32x4*)(pos + p * 1024 + c);
+    if (r & 1) v[i] = (slab_sum<S>(slab, B, b, c) + *(const f32x4*)(bias + c)) + pe;
+    else v[i] = *(const f32x4*)(cls + c) + pe;
+    *(f32x4*)(x + (size_t)r * 1024 + c) = v[i];
+  }
+  ln_row_store<T>(v, g, bta, y + (size_t)r * 1024, lane);
+}
+
+// LayerNorm(1024, eps 1e-5) (PreNorm, cvit.py:13-20): one wave per row,
+// fp32 statistics, 16-bit output feeding the next GEMM.
+template <class T>
+__global__ __launch_bounds__(64) void layernorm_rows(const float* __restrict__ x, const float* __restrict__ g,
+                                                     const float* __restrict__ bta, uint16_t* __restrict__ y,
+                                                     int R) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const float* xr = x + (size_t)row * 1024;
+  f32x4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = *(const f32x4*)(xr + i * 256 + lane * 4);
+  ln_row_store<T>(v, g, bta, y + (size_t)row * 1024, lane);
+}
+
+// Residual add of a split-K projection + the next PreNorm LayerNorm, fused:
+//   x[r] += (sum_s slab[s][r]) + bias      (Residual, cvit.py:10-11)
+//   y[r]  = LayerNorm(x[r]) * g + b -> 16-bit (PreNorm, cvit.py:19-20)
+// One 64-thread workgroup per row (R = 2B = 512 workgroups).
+template <class T, int S>
+__global__ __launch_bounds__(64) void resid_layernorm(float* __restrict__ x, const float* __restrict__ slab,
+                                                      const float* __restrict__ bias, const float* __restrict__ g,
+                                                      const float* __restrict__ bta, uint16_t* __restrict__ y,
+                                                      int R) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  float* xr = x + (size_t)row * 1024;
+  f32x4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = i * 256 + lane * 4;
+    v[i] = (slab_sum<S>(slab, R, row, c) + *(const f32x4*)(bias + c)) + *(const f32x4*)(xr + c);
+    *(f32x4*)(xr + c) = v[i];
+  }
+  ln_row_store<T>(v, g, bta, y + (size_t)row * 1024, lane);
 }
 
 // After the last layer only the CLS rows matter (cvit.py:177): finish their
 // residual add from the FF2 split-K partials and convert to 16-bit for the head.
-template <class T>
-__global__ __launch_bounds__(256) void resid_cls(const float* __restrict__ x, const float* __restrict__ slab, int S,
+template <class T, int S>
+__global__ __launch_bounds__(256) void resid_cls(const float* __restrict__ x, const float* __restrict__ slab,
                                                  const float* __restrict__ bias, uint16_t* __restrict__ c, int B) {
   const int i = blockIdx.x * 256 + threadIdx.x;  // over B*256 float4 groups
   if (i >= B * 256) return;
   const int b = i >> 8, col = (i & 255) * 4, row = 2 * b, R = 2 * B;
-  f32x4 p = *(const f32x4*)(slab + (size_t)row * 1024 + col);
-  for (int k = 1; k < S; ++k) p += *(const f32x4*)(slab + ((size_t)k * R + row) * 1024 + col);
-  const f32x4 v = (p + *(const f32x4*)(bias + col)) + *(const f32x4*)(x + (size_t)row * 1024 + col);
+  const f32x4 v = (slab_sum<S>(slab, R, row, col) + *(const f32x4*)(bias + col)) + *(const f32x4*)(x + (size_t)row * 1024 + col);
   u16x4 o;
 #pragma unroll
   for (int j = 0; j < 4; ++j) o[j] = T::from_f32(v[j]);
@@ -436,34 +437,68 @@ hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uin
   return launch_gemm_t<F16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, variant, st);
 }
 
-hipError_t launch_embed_finalize(const float* slab, int S, int B, const float* bias, const float* cls,
-                                 const float* pos, const int32_t* pidx, float* x, int* err, hipStream_t st) {
-  embed_finalize<<<B, 256, 0, st>>>(slab, S, B, bias, cls, pos, pidx, x, err);
+template <class T>
+static hipError_t embed_ln_t(const float* slab, int S, int B, const float* bias, const float* cls, const float* pos,
+                             const int32_t* pidx, float* x, const float* g, const float* bt, uint16_t* y, int* err,
+                             hipStream_t st) {
+  switch (S) {
+    case 7: embed_finalize_ln<T, 7><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err); break;
+    case 14: embed_finalize_ln<T, 14><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err); break;
+    case 28: embed_finalize_ln<T, 28><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
+}
+
+hipError_t launch_embed_finalize_ln(int dtype, const float* slab, int S, int B, const float* bias, const float* cls,
+                                    const float* pos, const int32_t* pidx, float* x, const float* g, const float* bt,
+                                    uint16_t* y, int* err, hipStream_t st) {
+  if (dtype == 0) return embed_ln_t<BF16>(slab, S, B, bias, cls, pos, pidx, x, g, bt, y, err, st);
+  return embed_ln_t<F16>(slab, S, B, bias, cls, pos, pidx, x, g, bt, y, err, st);
 }
 
 hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,
                             hipStream_t st) {
-  dim3 grid((R + 3) / 4);
-  if (dtype == 0) layernorm_rows<BF16><<<grid, 256, 0, st>>>(x, g, b, y, R);
-  else layernorm_rows<F16><<<grid, 256, 0, st>>>(x, g, b, y, R);
+  if (dtype == 0) layernorm_rows<BF16><<<R, 64, 0, st>>>(x, g, b, y, R);
+  else layernorm_rows<F16><<<R, 64, 0, st>>>(x, g, b, y, R);
+  return hipGetLastError();
+}
+
+template <class T>
+static hipError_t resid_ln_t(float* x, const float* slab, int S, const float* bias, const float* g, const float* b,
+                             uint16_t* y, int R, hipStream_t st) {
+  switch (S) {
+    case 1: resid_layernorm<T, 1><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R); break;
+    case 2: resid_layernorm<T, 2><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R); break;
+    case 4: resid_layernorm<T, 4><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_resid_layernorm(int dtype, float* x, const float* slab, int S, const float* bias, const float* g,
-                                 const float* b, uint16_t* y, int R, hipStream_t st) {
-  dim3 grid((R + 3) / 4);
-  if (dtype == 0) resid_layernorm<BF16><<<grid, 256, 0, st>>>(x, slab, S, bias, g, b, y, R);
-  else resid_layernorm<F16><<<grid, 256, 0, st>>>(x, slab, S, bias, g, b, y, R);
+                                  const float* b, uint16_t* y, int R, hipStream_t st) {
+  if (dtype == 0) return resid_ln_t<BF16>(x, slab, S, bias, g, b, y, R, st);
+  return resid_ln_t<F16>(x, slab, S, bias, g, b, y, R, st);
+}
+
+template <class T>
+static hipError_t resid_cls_t(const float* x, const float* slab, int S, const float* bias, uint16_t* c, int B,
+                              hipStream_t st) {
+  dim3 grid(B);
+  switch (S) {
+    case 1: resid_cls<T, 1><<<grid, 256, 0, st>>>(x, slab, bias, c, B); break;
+    case 2: resid_cls<T, 2><<<grid, 256, 0, st>>>(x, slab, bias, c, B); break;
+    case 4: resid_cls<T, 4><<<grid, 256, 0, st>>>(x, slab, bias, c, B); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_resid_cls(int dtype, const float* x, const float* slab, int S, const float* bias, uint16_t* c, int B,
                             hipStream_t st) {
-  dim3 grid(B);
-  if (dtype == 0) resid_cls<BF16><<<grid, 256, 0, st>>>(x, slab, S, bias, c, B);
-  else resid_cls<F16><<<grid, 256, 0, st>>>(x, slab, S, bias, c, B);
-  return hipGetLastError();
+  if (dtype == 0) return resid_cls_t<BF16>(x, slab, S, bias, c, B, st);
+  return resid_cls_t<F16>(x, slab, S, bias, c, B, st);
 }
 
 hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipStream_t st) {
