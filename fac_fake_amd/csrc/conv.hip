@@ -75,8 +75,12 @@ __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, 
   }
 }
 
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL>
-__global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
+// HB: halo buffers (2: the next chunk's halo streams in during this chunk;
+// 1: it is loaded between chunks, exposed, which halves the halo LDS so that
+// OCC = 3 workgroups share a CU and hide each other's exposed loads — the
+// 112^2 layers, whose 1-2 chunks leave little to pipeline within a box).
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
@@ -98,7 +102,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
   constexpr int WSL = BN * CK;              // elements per tap slice
   constexpr int OPIX = POOL ? NPIX / 4 : NPIX;
   constexpr int OPS = BN + 8;
-  constexpr int OPER = 2 * HALO + 3 * WSL;           // halo double buffer + 3-slot weight ring
+  constexpr int OPER = HB * HALO + 3 * WSL;          // halo buffer(s) + 3-slot weight ring
   constexpr int OSTG = (POOL ? RT * 4 : RT * 16) * OPS;  // padded: epilogue writes unguarded
   constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
   static_assert(WM * WN == 4, "4 waves");
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
   // [256i + 64w, +64) straight into ring slot `slot`.
   constexpr int WPIECES = BN * CK / 8;
   constexpr int WPW = (WPIECES + 255) / 256;  // glds instructions per wave per slice
-  uint16_t* const wring = smem + 2 * HALO;
+  uint16_t* const wring = smem + HB * HALO;
   auto issue_w = [&](int slot, const uint16_t* src) {
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
@@ -208,8 +212,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
   for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(smem + abase[rt]);
 
   for (int c = 0; c < nchunks; ++c) {
-    const uint16_t* hb = smem + (c & 1) * HALO;
-    const uint16_t* hbn = smem + ((c + 1) & 1) * HALO;
+    if constexpr (HB == 1) {
+      if (c > 0) {  // every wave is past the previous chunk's last barrier
+        issue_halo(smem, c);
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+        for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(smem + abase[rt]);
+      }
+    }
+    const uint16_t* hb = smem + (HB == 2 ? (c & 1) * HALO : 0);
+    const uint16_t* hbn = smem + (HB == 2 ? ((c + 1) & 1) * HALO : 0);
     const bool next_h = c + 1 < nchunks;
     const uint16_t* wnext = wsrc + (size_t)(c * 9 + 2) * WSL;
     auto step = [&](auto tc) {
@@ -219,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
       // other halo buffer (on the last chunk a dummy re-read of this chunk);
       // glds are LDS writes, so the compiler keeps them in program order
       issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
-      if (t == 0) issue_halo(smem + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
+      if (HB == 2 && t == 0) issue_halo(smem + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
       const uint16_t* wb = wring + (t % 3) * WSL;
       u16x8 bfr[CTW];
 #pragma unroll
@@ -230,7 +242,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
       for (int rt = 0; rt < RTW; ++rt) {
 #pragma unroll
         for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
-        fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
+        // (HB = 1: the next chunk's tap-0 fragments are read once its halo is in)
+        if (HB == 2 || t < 8) fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
       }
       __builtin_amdgcn_sched_group_barrier(0x100, CTW, 0);
 #pragma unroll
@@ -241,7 +254,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_bn_relu(const uint16_t* __rest
       // Retire slice s+1 (and at t = 1 the next halo), leaving younger glds in
       // flight; wait + barrier in ONE asm statement, so no LDS access can be
       // scheduled between this wave's wait and the workgroup barrier.
-      constexpr int N = WPW + (t <= 1 ? HPW : 0);
+      constexpr int N = WPW + (HB == 2 && t <= 1 ? HPW : 0);
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
       __builtin_amdgcn_sched_barrier(0);
     };
@@ -396,7 +409,8 @@ namespace fac {
 // Per-resolution kernel configuration (box TH x TW, BN output channels per
 // workgroup, WM x WN wave grid); must agree with the weight packing in
 // cvit_abi.hip, which asks conv_block_n() for BN.
-//   112: 16x16 box, BN  64, 4x1 waves (256 rows, no padding)
+//   112: 16x16 box, BN  64, 4x1 waves (256 rows, no padding), 1 halo buffer,
+//        4 workgroups per CU
 //    56:  8x28 box, BN 128, 2x2 waves (224 rows, no padding)
 //    28:  4x28 box, BN 256, 1x4 waves (112 rows, no padding)
 //    14: 14x14 box, BN 128, 1x4 waves (208 rows for 196 pixels)
@@ -411,14 +425,16 @@ int conv_block_n(int H) {
   }
 }
 
-template <class T, int TH, int TW, int BN, int WM, int WN>
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2>
 static void launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                        int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if (pool)
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC>
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
   else
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC>
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
 }
 
 template <class T>
@@ -427,7 +443,9 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
   if (W != H) return hipErrorInvalidValue;
   switch (H) {
     case 224: launch_box<T, 16, 16, 32, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
-    case 112: launch_box<T, 16, 16, 64, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
+    // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
+    case 112: launch_box<T, 16, 16, 64, 4, 1, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     case 14: launch_box<T, 14, 14, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
