@@ -88,6 +88,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     ap.add_argument("--stem-chunk", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="synchronous steps (hipGraph of one forward) instead of the software pipeline "
+                         "that overlaps batch k's encoder with batch k+1's conv stack")
     ap.add_argument("--no-fuse", action="store_true", help="unfused conv1..conv3 (A/B of the fused 224 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
@@ -123,6 +126,7 @@ def main():
     crops = torch.from_numpy(make_crops(B, seed=3 + rank)).to(dev)      # synthetic, resident in HBM
     pidx = (torch.arange(B, device=dev) % 32).to(torch.int32)
     logits = torch.empty(B, 2, dtype=torch.float32, device=dev)
+    logits_pp = [torch.empty(B, 2, dtype=torch.float32, device=dev) for _ in range(2)]  # pipelined steps
     score = torch.empty((), dtype=torch.float32, device=dev)
     gathered = torch.empty(world * B, 2, dtype=torch.float32, device=dev)
     stream = torch.cuda.Stream(dev)
@@ -131,8 +135,9 @@ def main():
         _lib.check(lib.fac_forward_nhwc_u8(ctx, crops.data_ptr(), B, pidx.data_ptr(), logits.data_ptr(), None,
                                            s.cuda_stream), ctx, "forward")
 
+    pipelined = not args.no_pipeline
     graph = None
-    if not args.no_graph:
+    if not args.no_graph and not pipelined:
         try:
             stream.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(stream):
@@ -146,7 +151,41 @@ def main():
             print(f"[bench] graph capture failed, running eager: {e}", file=sys.stderr)
             graph = None
 
+    kstep = [0]
+
+    def step_pipelined():
+        # batch k: conv stack on `stream`, encoder + head (+ score at N=1) on the
+        # context's tail stream; at N>1 the logits of batch k-1 are gathered
+        # (RCCL) and scored one step later, so the gather never stalls the
+        # conv stack of the next batch
+        k = kstep[0]
+        kstep[0] += 1
+        lg = logits_pp[k & 1]
+        with torch.cuda.stream(stream):
+            _lib.check(lib.fac_forward_nhwc_u8_pipelined(ctx, crops.data_ptr(), B, pidx.data_ptr(), lg.data_ptr(),
+                                                         None, score.data_ptr() if world == 1 else None,
+                                                         stream.cuda_stream), ctx, "forward_pipelined")
+            if world > 1 and k > 0:
+                _lib.check(lib.fac_pipeline_join(ctx, 1, stream.cuda_stream), ctx, "join")
+                gather_score(logits_pp[(k - 1) & 1])
+
+    def gather_score(lg):
+        dist.all_gather_into_tensor(gathered, lg)
+        _lib.check(lib.fac_video_score(gathered.data_ptr(), world * B, score.data_ptr(), stream.cuda_stream),
+                   None, "video_score")
+
+    def drain():
+        # every enqueued batch complete (and, at N>1, the last one gathered + scored)
+        if not pipelined:
+            return
+        with torch.cuda.stream(stream):
+            _lib.check(lib.fac_pipeline_join(ctx, 0, stream.cuda_stream), ctx, "join")
+            if world > 1 and kstep[0] > 0:
+                gather_score(logits_pp[(kstep[0] - 1) & 1])
+
     def step():
+        if pipelined:
+            return step_pipelined()
         with torch.cuda.stream(stream):
             if graph is not None:
                 graph.replay()
@@ -162,6 +201,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    drain()
+    kstep[0] = 0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -169,6 +210,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -218,7 +260,7 @@ def main():
                    "model": "CViT(224,7,2,512,1024,6,8,2048)", "global_batch": world * B, "seq_len": 2,
                    "parallelism": f"frame-sharded x{world}" + (" + RCCL logit all-gather" if world > 1 else ""),
                    "graph": graph is not None, "stem_chunk": args.stem_chunk,
-                   "fused_stem224": not args.no_fuse, **({"options": args.opt} if args.opt else {})},
+                   "fused_stem224": not args.no_fuse, "pipelined": pipelined, **({"options": args.opt} if args.opt else {})},
         "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
         "roofline": {"bound": "mfma", "kernel": dom_name,
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

@@ -109,6 +109,15 @@ struct fac_ctx {
   // and the split-K factor of the two N=1024 projections (to_out, FF2)
   int gemm_var[6] = {-1, -1, -1, -1, -1, -1};  // patch, qkv, out, ff1, ff2, head
   int proj_splits = 4;
+  // software pipeline across batches (fac_forward_nhwc_u8_pipelined): batch k's
+  // conv stack writes stem buffer k&1 on the caller's stream; its encoder +
+  // head run on tail_st, ordered by ev_conv[k&1] / ev_tail[k&1]
+  hipStream_t tail_st = nullptr;
+  hipEvent_t ev_conv[2] = {nullptr, nullptr}, ev_tail[2] = {nullptr, nullptr};
+  bool tail_pending[2] = {false, false};
+  int pipe_k = 0;
+  int tail_priority = 1;  // option "tail_priority": 1 = high-priority tail stream
+  uint16_t* stem_out2 = nullptr;
   int num_cu = 256;
   uint16_t *act0 = nullptr, *act1 = nullptr, *deep0 = nullptr, *deep1 = nullptr, *stem_out = nullptr, *xn = nullptr,
            *o = nullptr, *hbuf = nullptr, *cbuf = nullptr;
@@ -146,7 +155,7 @@ hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, ui
 }
 
 struct WsLayout {
-  size_t act, deep, stem, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
+  size_t act, deep, stem, stem2, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
   int cb;  // crops the high-res activation buffers hold (stem chunk)
 };
 
@@ -167,6 +176,7 @@ WsLayout layout(int B, int chunk) {
   L.act = off; off += 2 * al((size_t)cb * kActElems * 2);
   L.deep = off; off += 2 * al((size_t)B * kDeepElems * 2);
   L.stem = off; off += al((size_t)B * kPatchDim * 2);
+  L.stem2 = off; off += al((size_t)B * kPatchDim * 2);
   L.slab = off; off += al(S * kDim * 4);
   L.x = off; off += al((size_t)2 * B * kDim * 4);
   L.xn = off; off += al((size_t)2 * B * kDim * 2);
@@ -203,6 +213,7 @@ int ensure_ws(fac_ctx* c, int B) {
   c->deep1 = (uint16_t*)(base + L.deep + dhalf);
   c->cap_chunk = L.cb;
   c->stem_out = (uint16_t*)(base + L.stem);
+  c->stem_out2 = (uint16_t*)(base + L.stem2);
   c->slab = (float*)(base + L.slab);
   c->x = (float*)(base + L.x);
   c->xn = (uint16_t*)(base + L.xn);
@@ -386,18 +397,30 @@ struct Prof {
   std::vector<int> stage;
 };
 
+int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, float* logits, float* probs,
+              hipStream_t st, Prof* prof);
+
+// The synchronous forward on `stream`: conv stack -> stem_dst (default the
+// context's stem buffer 0), then (unless conv_only) the encoder and head.
 int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
                  void* stream, Prof* prof = nullptr, int stop_after = -1, uint16_t* feat_out = nullptr,
-                 const uint16_t* stem_in = nullptr) {
+                 const uint16_t* stem_in = nullptr, uint16_t* stem_dst = nullptr, bool conv_only = false) {
   using namespace fac;
   if (!c) return FAC_ERR_ARG;
   if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "forward before fac_load_weights");
-  if (B <= 0 || (!in && !stem_in) || (stop_after < 0 && (!pidx || !logits)))
+  if (B <= 0 || (!in && !stem_in) || (stop_after < 0 && !conv_only && (!pidx || !logits)))
     return set_err(c, FAC_ERR_ARG, "bad forward arguments");
   DevGuard g(c->device);
   int rc = ensure_ws(c, B);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (!stem_dst) {
+    // a synchronous forward shares the encoder workspace with pipelined
+    // tails still in flight: order it after them
+    stem_dst = c->stem_out;
+    for (int i = 0; i < 2; ++i)
+      if (c->tail_pending[i]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[i], 0));
+  }
   const int dt = c->dtype;
   const int chunk = std::min(B, c->cap_chunk);
 #define MARK(sid)                                  \
@@ -470,7 +493,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     }
     for (int l = kLastChunked + 1; l < 16; ++l) {
       const ConvLayer& L = c->conv[l];
-      uint16_t* dst = (l == 15) ? c->stem_out : nxt;
+      uint16_t* dst = (l == 15) ? stem_dst : nxt;
       HIP_TRY(c, run_conv(c, L, cur, dst, B, st));
       MARK(l + 1);
       if (stop_after == l + 1) {
@@ -480,8 +503,29 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
       std::swap(cur, nxt);
     }
   }
+  if (conv_only) return FAC_OK;
+  return tail_impl(c, stem_in ? stem_in : stem_dst, B, pidx, logits, probs, st, prof);
+#undef MARK
+}
+
+// Patch embedding, the 6 encoder layers and the head on `st`, from the conv
+// stack's output `stem` [B,7,7,512] (cvit.py:171-179).
+int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, float* logits, float* probs,
+              hipStream_t st, Prof* prof) {
+  using namespace fac;
+  const int dt = c->dtype;
+#define MARK(sid)                                  \
+  do {                                             \
+    if (prof) {                                    \
+      hipEvent_t mk_;                              \
+      HIP_TRY(c, hipEventCreate(&mk_));            \
+      prof->ev.push_back(mk_);                     \
+      prof->stage.push_back(sid);                  \
+      HIP_TRY(c, hipEventRecord(mk_, st));         \
+    }                                              \
+  } while (0)
   const int S = patch_splits(B);
-  HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, stem_in ? stem_in : c->stem_out, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
+  HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, stem, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
                          kPatchDim, S, st, c->gemm_var[0]));
   // residual stream rows + layer 0's PreNorm LayerNorm in one pass
   HIP_TRY(c, launch_embed_finalize_ln(dt, c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->tl[0].ln1_g,
@@ -585,6 +629,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
       c->gemm_var[i] = value;
       return FAC_OK;
     }
+  if (k == "tail_priority") {
+    if (c->tail_st) return set_err(c, FAC_ERR_ARG, "tail_priority must be set before the first pipelined forward");
+    c->tail_priority = value != 0;
+    return FAC_OK;
+  }
   if (k == "proj_splits") {
     if (value != 1 && value != 2 && value != 4) return set_err(c, FAC_ERR_ARG, "proj_splits must be 1, 2 or 4");
     c->proj_splits = value;
@@ -601,6 +650,58 @@ int fac_forward_nchw_f32(fac_ctx* c, const float* d_in, int B, const int32_t* d_
 int fac_forward_nhwc_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,
                         void* stream) {
   return forward_impl(c, d_in, true, B, d_pos, d_logits, d_probs, stream);
+}
+
+int fac_forward_nhwc_u8_pipelined(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits,
+                                  float* d_probs, float* d_score, void* stream) {
+  if (!c) return FAC_ERR_ARG;
+  if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "forward before fac_load_weights");
+  if (!d_in || !d_pos || !d_logits || B <= 0) return set_err(c, FAC_ERR_ARG, "bad pipelined forward arguments");
+  DevGuard g(c->device);
+  if (!c->tail_st) {
+    // the encoder's short, latency-bound kernels get the higher priority, so
+    // the dispatcher slots their workgroups in as the conv stack's retire
+    int lo = 0, hi = 0;
+    HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(c, hipStreamCreateWithPriority(&c->tail_st, hipStreamNonBlocking, c->tail_priority ? hi : lo));
+    for (int i = 0; i < 2; ++i) {
+      HIP_TRY(c, hipEventCreateWithFlags(&c->ev_conv[i], hipEventDisableTiming));
+      HIP_TRY(c, hipEventCreateWithFlags(&c->ev_tail[i], hipEventDisableTiming));
+    }
+  }
+  if (B > c->cap_B && (c->tail_pending[0] || c->tail_pending[1]))
+    HIP_TRY(c, hipStreamSynchronize(c->tail_st));  // the workspace is about to be reallocated
+  int rc = ensure_ws(c, B);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const int k = c->pipe_k & 1;
+  uint16_t* stem = k ? c->stem_out2 : c->stem_out;
+  // stem buffer k was last read by the tail of batch k-2
+  if (c->tail_pending[k]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[k], 0));
+  rc = forward_impl(c, d_in, true, B, nullptr, nullptr, nullptr, stream, nullptr, -1, nullptr, nullptr, stem, true);
+  if (rc) return rc;
+  HIP_TRY(c, hipEventRecord(c->ev_conv[k], st));
+  HIP_TRY(c, hipStreamWaitEvent(c->tail_st, c->ev_conv[k], 0));
+  rc = tail_impl(c, stem, B, d_pos, d_logits, d_probs, c->tail_st, nullptr);
+  if (rc) return rc;
+  if (d_score) HIP_TRY(c, fac::launch_video_score(d_logits, B, d_score, c->tail_st));
+  HIP_TRY(c, hipEventRecord(c->ev_tail[k], c->tail_st));
+  c->tail_pending[k] = true;
+  c->pipe_k++;
+  return FAC_OK;
+}
+
+int fac_pipeline_join(fac_ctx* c, int keep, void* stream) {
+  if (!c || keep < 0) return FAC_ERR_ARG;
+  if (!c->tail_st) return FAC_OK;
+  DevGuard g(c->device);
+  // the batches enqueued, oldest first: pipe_k-2, pipe_k-1 (slots (pipe_k-2)&1, (pipe_k-1)&1)
+  for (int age = 2; age > keep; --age) {
+    const int k = (c->pipe_k - age) & 1;
+    if (c->pipe_k - age >= 0 && c->tail_pending[k])
+      HIP_TRY(c, hipStreamWaitEvent((hipStream_t)stream, c->ev_tail[k], 0));
+  }
+  return FAC_OK;
 }
 
 int fac_debug_gemm(fac_ctx* c, int epi, const uint16_t* d_a, const uint16_t* d_w, const float* d_bias, void* d_out,
@@ -675,6 +776,13 @@ void fac_destroy(fac_ctx* c) {
   {
     DevGuard g(c->device);
     (void)hipDeviceSynchronize();
+    if (c->tail_st) {
+      (void)hipStreamDestroy(c->tail_st);
+      for (int i = 0; i < 2; ++i) {
+        (void)hipEventDestroy(c->ev_conv[i]);
+        (void)hipEventDestroy(c->ev_tail[i]);
+      }
+    }
     for (void* p : c->weights) (void)hipFree(p);
     if (c->ws) (void)hipFree(c->ws);
   }

@@ -83,6 +83,21 @@ int fac_forward_nchw_f32(fac_ctx* ctx, const float* d_in, int B, const int32_t* 
 int fac_forward_nhwc_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
                         float* d_probs, void* stream);
 
+/* Software-pipelined forward for streams of batches (a video-scoring
+ * server; bench.py's default mode).  Enqueues batch k's conv stack on
+ * `stream` (into one of two context-owned stem buffers) and its patch
+ * embedding + encoder + head (+ video score into d_score if non-NULL) on a
+ * context-owned stream that waits only for that conv stack, so batch k's
+ * latency-bound encoder overlaps batch k+1's conv stack.  Same arithmetic as
+ * fac_forward_nhwc_u8 (bit-identical logits).  d_in may be reused once
+ * `stream` has passed this call; d_pos / d_logits / d_probs / d_score must
+ * stay valid, and are complete, only after fac_pipeline_join.
+ * fac_pipeline_join: makes `stream` wait for every enqueued batch except the
+ * `keep` most recent ones (keep = 0: all; keep = 1: all but the last). */
+int fac_forward_nhwc_u8_pipelined(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index,
+                                  float* d_logits, float* d_probs, float* d_score, void* stream);
+int fac_pipeline_join(fac_ctx* ctx, int keep, void* stream);
+
 /* Test/measurement entry points ------------------------------------------
  * fac_debug_features_u8: run conv1..conv{layer+1} (layer 0..16) on uint8
  * crops and copy that block's NHWC 16-bit output (after ReLU, and after the

@@ -384,3 +384,44 @@ def test_gemm_variants_vs_torch_fp32(models, dt, variant):
     r = torch.nn.functional.gelu(ref + bias).to(tdt).float()
     ulp = torch.finfo(tdt).eps * r.abs().clamp_min(1e-3)
     assert ((o - r).abs() <= ulp + 2 * bound).all()
+
+
+def test_pipelined_forward_matches_synchronous(models):
+    """fac_forward_nhwc_u8_pipelined (batch k's encoder on the context's
+    stream, overlapping batch k+1's conv stack) gives bit-identical logits,
+    probabilities and video scores to the synchronous forward, over 5
+    back-to-back batches of different sizes and a synchronous forward issued
+    in the middle of the pipeline."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models["bf16"]
+    ctx = m._ctx
+    sizes = [64, 64, 17, 64, 40]
+    batches = [torch.from_numpy(make_crops(n, seed=100 + i)).to(DEV) for i, n in enumerate(sizes)]
+    slots = [(torch.arange(n, device=DEV) % 32).to(torch.int32) for n in sizes]
+    ref = []
+    for x, p in zip(batches, slots):
+        ref.append(m.forward_u8(x, pos_index=p.cpu()).cpu())
+    s = torch.cuda.Stream(DEV)
+    outs = [torch.full((n, 2), float("nan"), device=DEV) for n in sizes]
+    probs = [torch.full((n, 2), float("nan"), device=DEV) for n in sizes]
+    scores = [torch.full((), float("nan"), device=DEV) for _ in sizes]
+    with torch.cuda.stream(s):
+        for i, (x, p) in enumerate(zip(batches, slots)):
+            _lib.check(lib.fac_forward_nhwc_u8_pipelined(ctx, x.data_ptr(), sizes[i], p.data_ptr(),
+                                                         outs[i].data_ptr(), probs[i].data_ptr(),
+                                                         scores[i].data_ptr(), s.cuda_stream), ctx, "pipelined")
+            if i == 2:  # a synchronous forward in the middle orders itself after the pending tails
+                mid = m.forward_u8(batches[0], pos_index=slots[0].cpu())
+        _lib.check(lib.fac_pipeline_join(ctx, 0, s.cuda_stream), ctx, "join")
+    torch.cuda.synchronize()
+    assert torch.equal(mid.cpu(), ref[0])
+    for i in range(len(sizes)):
+        assert torch.equal(outs[i].cpu(), ref[i]), i
+        assert torch.equal(probs[i].cpu(), torch.sigmoid(ref[i]).float()) or \
+            torch.allclose(probs[i].cpu(), torch.sigmoid(ref[i]), rtol=0, atol=1e-6)
+        sc = torch.empty((), device=DEV)
+        _lib.check(lib.fac_video_score(outs[i].data_ptr(), sizes[i], sc.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream), None, "video_score")
+        torch.cuda.synchronize()
+        assert torch.equal(scores[i].cpu(), sc.cpu()), i

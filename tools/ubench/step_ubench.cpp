@@ -12,22 +12,23 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
-template <int PTW, int CTW, int MODE, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 1) void step_kernel(float* out, int steps, long long* cyc) {
+template <int PTW, int CTW, int MODE, int WAVES, int WGS = 1>
+__global__ __launch_bounds__(WAVES * 64, WGS) void step_kernel(float* out, int steps, long long* cyc) {
   // MODE bit0: LDS reads, bit1: barrier each step, bit2: pipelined reads (next-step frags),
   // bit3: pipelined + forced interleave (1 read per MFMA group), bit4: pipelined + all
   // reads first, bit5: conflict-free B addresses
-  __shared__ __attribute__((aligned(16))) unsigned short lds[65536];
+  constexpr int LDSN = 65536 / WGS;
+  __shared__ __attribute__((aligned(16))) unsigned short lds[LDSN];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 65536; i += blockDim.x) lds[i] = (unsigned short)(i * 7);
+  for (int i = threadIdx.x; i < LDSN; i += blockDim.x) lds[i] = (unsigned short)(i * 7);
   __syncthreads();
   int pb[PTW];
 #pragma unroll
   for (int p = 0; p < PTW; ++p)
-    pb[p] = (MODE & 32) ? ((lane >> 4) * 16 + p * 64 + (lane & 15)) * 16 : ((lane >> 4) * 392 + p * 16 + (lane & 15)) * 16 + wave * 1024;
+    pb[p] = (MODE & 32) ? ((lane >> 4) * 16 + p * 64 + (lane & 15)) * 16 : ((lane >> 4) * 392 + p * 16 + (lane & 15)) * 16 + (wave & 3) * 1024;
   int wb[CTW];
 #pragma unroll
-  for (int c = 0; c < CTW; ++c) wb[c] = 98304 + ((lane >> 4) * 128 + c * 16 + (lane & 15)) * 16;
+  for (int c = 0; c < CTW; ++c) wb[c] = LDSN * 2 - 32768 + ((lane >> 4) * 128 + c * 16 + (lane & 15)) * 16;
   f32x4 acc[PTW][CTW];
 #pragma unroll
   for (int p = 0; p < PTW; ++p)
@@ -93,19 +94,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void step_kernel(float* out, int ste
 #pragma unroll
     for (int c = 0; c < CTW; ++c) s += acc[p][c][0] + acc[p][c][1] + acc[p][c][2] + acc[p][c][3];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  if (threadIdx.x == 0 && blockIdx.x < 256) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int PTW, int CTW, int MODE, int WAVES>
+template <int PTW, int CTW, int MODE, int WAVES, int WGS = 1>
 void run(const char* name, float* out, long long* cyc) {
   const int steps = 2000;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  step_kernel<PTW, CTW, MODE, WAVES><<<256, WAVES * 64>>>(out, 10, cyc);
+  step_kernel<PTW, CTW, MODE, WAVES, WGS><<<256 * WGS, WAVES * 64>>>(out, 10, cyc);
   hipDeviceSynchronize();
   hipEventRecord(e0);
-  step_kernel<PTW, CTW, MODE, WAVES><<<256, WAVES * 64>>>(out, steps, cyc);
+  step_kernel<PTW, CTW, MODE, WAVES, WGS><<<256 * WGS, WAVES * 64>>>(out, steps, cyc);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -116,7 +117,7 @@ void run(const char* name, float* out, long long* cyc) {
   for (auto v : h) avg += v;
   avg /= 256;
   const double ns_per_step = ms * 1e6 / steps;
-  const int mfma_per_simd = PTW * CTW * (WAVES / 4);
+  const int mfma_per_simd = PTW * CTW * (WAVES / 4) * WGS;
   printf("%-34s ns/step %7.1f  (=%6.0f cyc @2.4GHz; MFMA floor %5d cyc, %.0f%%)  memtime/step %.1f\n", name,
          ns_per_step, ns_per_step * 2.4, mfma_per_simd * 16, 100.0 * mfma_per_simd * 16 / (ns_per_step * 2.4),
          avg / steps);
@@ -129,18 +130,13 @@ int main() {
   hipMalloc(&cyc, 256 * 8);
   run<13, 2, 0, 8>("8w 13x2 mfma only", out, cyc);
   run<13, 2, 3, 8>("8w 13x2 mfma+lds+barrier", out, cyc);
-  run<13, 2, 3 + 32, 8>("8w 13x2 mfma+lds+barrier cf", out, cyc);
   run<13, 2, 6 + 8, 8>("8w 13x2 pipe interleave", out, cyc);
-  run<13, 2, 6 + 8 + 32, 8>("8w 13x2 pipe interleave cf", out, cyc);
-  run<13, 2, 6 + 16, 8>("8w 13x2 pipe reads-first", out, cyc);
-  run<13, 2, 6 + 16 + 32, 8>("8w 13x2 pipe reads-first cf", out, cyc);
-  run<7, 4, 3, 8>("8w 7x4 mfma+lds+barrier", out, cyc);
-  run<7, 4, 6 + 8, 8>("8w 7x4 pipe interleave", out, cyc);
-  run<7, 4, 6 + 16, 8>("8w 7x4 pipe reads-first", out, cyc);
-  run<7, 4, 6 + 16 + 32, 8>("8w 7x4 pipe reads-first cf", out, cyc);
-  run<13, 4, 0, 4>("4w 13x4 mfma only", out, cyc);
-  run<13, 4, 6 + 8, 4>("4w 13x4 pipe interleave", out, cyc);
-  run<13, 4, 6 + 16, 4>("4w 13x4 pipe reads-first", out, cyc);
-  run<7, 8, 6 + 16 + 32, 4>("4w 7x8 pipe reads-first cf", out, cyc);
+  run<13, 2, 0, 4, 2>("2x4w 13x2 mfma only", out, cyc);
+  run<13, 2, 3, 4, 2>("2x4w 13x2 mfma+lds+barrier", out, cyc);
+  run<13, 2, 6 + 8, 4, 2>("2x4w 13x2 pipe interleave", out, cyc);
+  run<7, 4, 3, 4, 2>("2x4w 7x4 mfma+lds+barrier", out, cyc);
+  run<7, 4, 6 + 8, 4, 2>("2x4w 7x4 pipe interleave", out, cyc);
+  run<4, 4, 3, 4, 2>("2x4w 4x4 mfma+lds+barrier", out, cyc);
+  run<4, 4, 6 + 8, 4, 2>("2x4w 4x4 pipe interleave", out, cyc);
   return 0;
 }
