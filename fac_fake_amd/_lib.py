@@ -49,6 +49,8 @@ SIGNATURES = {
                                               ctypes.c_void_p]),
     "fac_check_device_errors": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "fac_video_score": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "fac_crop_resize_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_set_stem_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "fac_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     "fac_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
@@ -74,8 +76,18 @@ def load() -> ctypes.CDLL:
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                            " (the CViT path has no CPU fallback)")
     lib = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    overridden = "FAC_CVIT_LIB" in os.environ  # an older build for an A/B run may lack newer entry points
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if not overridden:
+                raise
+
+            def _missing(*_a, _n=name):
+                raise RuntimeError(f"{LIB_PATH} does not export {_n}")
+            setattr(lib, name, _missing)
+            continue
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -17,6 +17,15 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// ReLU as one v_max_i32 on the bit pattern (max(x, +0) for every non-NaN x,
+// -0 -> +0): fmaxf costs a NaN-canonicalising v_max plus the max.
+__device__ __forceinline__ float relu(float x) {
+  return __builtin_bit_cast(float, __builtin_elementwise_max(__builtin_bit_cast(int, x), 0));
+}
 
 struct BF16 {
   static constexpr int id = 0;
@@ -26,6 +35,12 @@ struct BF16 {
   }
   __device__ __forceinline__ static float to_f32(uint16_t x) {
     return __builtin_bit_cast(float, (uint32_t)x << 16);
+  }
+  // 4 floats -> 4 x 16-bit, round-to-nearest-even, two v_cvt_pk_bf16_f32
+  __device__ __forceinline__ static u16x4 pack4(f32x4 v) {
+    const bf16x2 lo = __builtin_convertvector((f32x2){v[0], v[1]}, bf16x2);
+    const bf16x2 hi = __builtin_convertvector((f32x2){v[2], v[3]}, bf16x2);
+    return __builtin_bit_cast(u16x4, __builtin_shufflevector(lo, hi, 0, 1, 2, 3));
   }
   __device__ __forceinline__ static f32x4 mfma(u16x8 a, u16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
@@ -41,6 +56,12 @@ struct F16 {
   }
   __device__ __forceinline__ static float to_f32(uint16_t x) {
     return (float)__builtin_bit_cast(_Float16, x);
+  }
+  // 4 floats -> 4 x 16-bit, round-to-nearest-even, two v_cvt_pk_f16_f32
+  __device__ __forceinline__ static u16x4 pack4(f32x4 v) {
+    const f16x2 lo = __builtin_convertvector((f32x2){v[0], v[1]}, f16x2);
+    const f16x2 hi = __builtin_convertvector((f32x2){v[2], v[3]}, f16x2);
+    return __builtin_bit_cast(u16x4, __builtin_shufflevector(lo, hi, 0, 1, 2, 3));
   }
   __device__ __forceinline__ static f32x4 mfma(u16x8 a, u16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),

@@ -283,12 +283,12 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       if constexpr (POOL) {
         const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
         const int w = (wm * RTW + rt) * 4 + (lane >> 4);
-        ostg[w * OPS + nl] = T::from_f32(fmaxf(mx + bv, 0.f));
+        ostg[w * OPS + nl] = T::from_f32(relu(mx + bv));
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int m = (wm * RTW + rt) * 16 + (lane >> 4) * 4 + j;
-          ostg[m * OPS + nl] = T::from_f32(fmaxf(v[j] + bv, 0.f));
+          ostg[m * OPS + nl] = T::from_f32(relu(v[j] + bv));
         }
       }
     }
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void conv1_bn_relu(const void* __restrict__ in
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int m = (wave * 4 + rt) * 16 + (lane >> 4) * 4 + j;
-        ostg[m * OPS + nl] = T::from_f32(fmaxf(acc[rt][ct][j] + bv, 0.f));
+        ostg[m * OPS + nl] = T::from_f32(relu(acc[rt][ct][j] + bv));
       }
   }
   __syncthreads();

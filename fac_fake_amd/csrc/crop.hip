@@ -1,0 +1,73 @@
+// Face-crop preprocessing of config 3:
+// cvit_prediction.py:111-116 takes frame[top:bottom, left:right] of a BGR
+// video frame, cv2.resize(.., (224, 224), interpolation=cv2.INTER_AREA),
+// then cv2.cvtColor(RGB2BGR), i.e. a channel swap that makes the crop RGB.
+//
+// INTER_AREA is an area-weighted average: output pixel o of an n-pixel span
+// resized to 224 covers the source interval [o*n/224, (o+1)*n/224), and each
+// source pixel contributes its overlap with that interval.  In units of
+// 1/224 pixel the interval is [o*n, (o+1)*n) and source pixel s covers
+// [224 s, 224 s + 224), so every weight is an exact integer overlap ov and
+//   out = round( sum_y sum_x ov_y ov_x src / (n_x n_y) )      (round half up)
+// in integer arithmetic: the GPU kernel and the numpy restatement
+// (oracle/crop_area.py) agree bit for bit.  cv2 itself evaluates the same
+// sum with float weights, so it may differ by one count on exact .5 ties
+// (cv2 is not in the image: parity with it is unpinned).
+// Boxes are clipped to the frame; an empty box gives a zero crop.
+#include "common.hpp"
+
+namespace fac {
+
+constexpr int kCrop = 224;
+
+// One thread per output pixel (all 3 channels); grid (crop, output row).
+__global__ __launch_bounds__(256) void crop_resize_area_u8(const uint8_t* __restrict__ frames, int n_frames, int H,
+                                                           int W, const int32_t* __restrict__ boxes,
+                                                           uint8_t* __restrict__ crops) {
+  const int n = blockIdx.x, oy = blockIdx.y, ox = threadIdx.x;
+  if (ox >= kCrop) return;
+  const int32_t* bx = boxes + 5 * n;  // (frame, left, top, right, bottom)
+  const int f = bx[0];
+  const int x0 = max(bx[1], 0), y0 = max(bx[2], 0), x1 = min(bx[3], W), y1 = min(bx[4], H);
+  uint8_t* dst = crops + (((size_t)n * kCrop + oy) * kCrop + ox) * 3;
+  const int nx = x1 - x0, ny = y1 - y0;
+  if (f < 0 || f >= n_frames || nx <= 0 || ny <= 0) {
+    dst[0] = dst[1] = dst[2] = 0;
+    return;
+  }
+  // interval of this output pixel in 1/224-pixel units, relative to the box
+  const int X0 = ox * nx, X1 = X0 + nx, Y0 = oy * ny, Y1 = Y0 + ny;
+  const int sx0 = X0 / kCrop, sx1 = (X1 - 1) / kCrop;  // covered source columns (inclusive)
+  const int sy0 = Y0 / kCrop, sy1 = (Y1 - 1) / kCrop;
+  const uint8_t* src = frames + (((size_t)f * H + y0) * W + x0) * 3;
+  long long acc0 = 0, acc1 = 0, acc2 = 0;
+  for (int sy = sy0; sy <= sy1; ++sy) {
+    const int ovy = min(Y1, (sy + 1) * kCrop) - max(Y0, sy * kCrop);
+    long long r0 = 0, r1 = 0, r2 = 0;
+    const uint8_t* row = src + (size_t)sy * W * 3;
+    for (int sx = sx0; sx <= sx1; ++sx) {
+      const int ovx = min(X1, (sx + 1) * kCrop) - max(X0, sx * kCrop);
+      const uint8_t* p = row + sx * 3;
+      r0 += ovx * p[0];
+      r1 += ovx * p[1];
+      r2 += ovx * p[2];
+    }
+    acc0 += ovy * r0;
+    acc1 += ovy * r1;
+    acc2 += ovy * r2;
+  }
+  const long long den = (long long)nx * ny;
+  // BGR source -> RGB crop (the cvtColor swap), round half up
+  dst[0] = (uint8_t)((2 * acc2 + den) / (2 * den));
+  dst[1] = (uint8_t)((2 * acc1 + den) / (2 * den));
+  dst[2] = (uint8_t)((2 * acc0 + den) / (2 * den));
+}
+
+hipError_t launch_crop_resize(const uint8_t* frames, int n_frames, int H, int W, const int32_t* boxes, int n_boxes,
+                              uint8_t* crops, hipStream_t st) {
+  if (n_boxes <= 0) return hipSuccess;
+  crop_resize_area_u8<<<dim3(n_boxes, kCrop), 256, 0, st>>>(frames, n_frames, H, W, boxes, crops);
+  return hipGetLastError();
+}
+
+}  // namespace fac

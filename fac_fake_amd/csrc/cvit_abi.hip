@@ -42,6 +42,8 @@ hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, fl
 hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, float* logits, float* probs, int B,
                            hipStream_t st);
 hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st);
+hipError_t launch_crop_resize(const uint8_t* frames, int n_frames, int H, int W, const int32_t* boxes, int n_boxes,
+                              uint8_t* crops, hipStream_t st);
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
                           hipStream_t st);
@@ -92,6 +94,7 @@ struct fac_ctx {
   std::string err;
   std::vector<void*> weights;  // all weight allocations
   uint16_t* conv1_w = nullptr;
+  uint16_t* conv1_wp = nullptr;  // conv1 weights in stem224's pixel-pair K order
   float* conv1_b = nullptr;
   ConvLayer conv[16];
   uint16_t* pe_w = nullptr;
@@ -313,6 +316,16 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
         for (int t = 0; t < 9; ++t)
           for (int cin = 0; cin < 3; ++cin) pk[(size_t)o * 64 + t * 4 + cin] = to16(c->dtype, wf(o, cin, t));
       if ((rc = upload(c, pk, &c->conv1_w))) return rc;
+      // stem224's K order: k = ((ky*2 + kx/2)*2 + kx%2)*4 + cin (kx = 3 and k >= 48
+      // zero), so one 16-byte lane chunk = two horizontally adjacent taps
+      std::vector<uint16_t> pp((size_t)32 * 64, 0);
+      for (int o = 0; o < 32; ++o)
+        for (int t = 0; t < 9; ++t)
+          for (int cin = 0; cin < 3; ++cin) {
+            const int ky = t / 3, kx = t % 3;
+            pp[(size_t)o * 64 + ((ky * 2 + kx / 2) * 2 + kx % 2) * 4 + cin] = to16(c->dtype, wf(o, cin, t));
+          }
+      if ((rc = upload(c, pp, &c->conv1_wp))) return rc;
       if ((rc = upload(c, bf, &c->conv1_b))) return rc;
     } else {
       ConvLayer& L = c->conv[i - 1];
@@ -451,7 +464,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     bool copied = false;  // stop_after's output already copied for this chunk
     if (c->fuse_stem224 && (stop_after < 0 || stop_after >= 2)) {
       // conv1..conv3 + pool in one kernel; the profile reports it as stage 0 (conv1)
-      HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_w, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
+      HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_wp, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
                                 c->conv[1].b, cur, nb, c->num_cu, st));
       MARK(0);
       l0 = 2;
@@ -787,6 +800,16 @@ void fac_destroy(fac_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
   }
   delete c;
+}
+
+int fac_crop_resize_u8(const uint8_t* d_frames, int n_frames, int H, int W, const int32_t* d_boxes, int n_boxes,
+                       uint8_t* d_crops, void* stream) {
+  if (!d_frames || !d_boxes || !d_crops || n_frames <= 0 || H <= 0 || W <= 0 || n_boxes < 0) return FAC_ERR_ARG;
+  if ((long long)n_frames * H * W * 3 >= (1ll << 40)) return FAC_ERR_SHAPE;
+  return fac::launch_crop_resize(d_frames, n_frames, H, W, d_boxes, n_boxes, d_crops, (hipStream_t)stream) ==
+                 hipSuccess
+             ? FAC_OK
+             : FAC_ERR_HIP;
 }
 
 const char* fac_version(void) { return "fac_cvit 0.1.0 (gfx950, MFMA 16x16x32 bf16/f16)"; }

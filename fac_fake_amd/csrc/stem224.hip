@@ -72,7 +72,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   uint16_t* const c1 = smem + OFF_C1;
   uint16_t* const c2 = smem + OFF_C2;
   uint16_t* const lut = smem + OFF_LUT;
-  uint16_t* const sin = c2;    // 22x38x4 input image: dead before conv2 writes c2
+  uint16_t* const sin = c2;    // 22x38 pixel-pair image (16 B slots): dead before conv2 writes c2
   uint16_t* const ostg = c1;   // 128 x (32+8) pooled tile: c1 is dead after conv2
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -115,8 +115,10 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     const int cy = m / C1W, cx = m - (m / C1W) * C1W;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int t = ks * 8 + 2 * g;  // taps t, t+1 (t+1 <= 9 only when t < 8)
-      in_off[i][ks] = ((cy + t / 3) * IW + cx + t % 3) * 4;
+      // lane chunk g of k-step ks = taps (ky, 2*kxp) and (ky, 2*kxp + 1): one
+      // pixel-pair slot; chunks past ky = 2 carry zero weights (any slot)
+      const int pr = ks * 4 + g, ky = pr < 6 ? pr >> 1 : 2, kxp = pr & 1;
+      in_off[i][ks] = ((cy + ky) * IW + cx + 2 * kxp) * 8;
     }
     c1_wr[i] = ((g >> 1) * P1 + cy * RP + cx) * 8 + (g & 1) * 4;  // + ct*2*P1*8 (channels 16ct+4g..)
   }
@@ -194,7 +196,12 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
           h[2] = T::from_f32(raw[k][2]);
         }
         h[3] = 0;
-        *(u16x4*)(sin + p * 4) = h;
+        // pixel-pair slot p = (pixel p, pixel p+1): left half of slot p, right
+        // half of slot p-1 (the last column's right half: zeros, zero weight)
+        const int ix = p - (p / IW) * IW;
+        *(u16x4*)(sin + p * 8) = h;
+        if (ix > 0) *(u16x4*)(sin + p * 8 - 4) = h;
+        if (ix == IW - 1) *(u16x4*)(sin + p * 8 + 4) = (u16x4)0;
       }
     }
     __syncthreads();
@@ -209,11 +216,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       f32x4 acc[2] = {bt1[0], bt1[1]};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int t0 = ks * 8 + 2 * g;
-        u16x4 lo = (u16x4)0, hi = (u16x4)0;
-        if (t0 < 9) lo = *(const u16x4*)(sin + in_off[i][ks]);
-        if (t0 + 1 < 9) hi = *(const u16x4*)(sin + in_off[i][ks] + ((t0 + 1) % 3 == 0 ? IW * 4 - 2 * 4 : 4));
-        const u16x8 p = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        const u16x8 p = *(const u16x8*)(sin + in_off[i][ks]);
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
           const u16x8 wf = *(const u16x8*)(sw1 + (ct * 16 + r16) * W1P + ks * 32 + g * 8);
@@ -228,9 +231,10 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       }
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        u16x4 o;
+        f32x4 r;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = T::from_f32(fmaxf(acc[ct][j], 0.f));
+        for (int j = 0; j < 4; ++j) r[j] = relu(acc[ct][j]);
+        u16x4 o = T::pack4(r);
         if (!inside) o = (u16x4)0;
         *(u16x4*)(c1 + c1_wr[i] + ct * 2 * P1 * 8) = o;
       }
@@ -274,9 +278,10 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         }
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) {
-          u16x4 o;
+          f32x4 r;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = T::from_f32(fmaxf(acc[i][ct][j], 0.f));
+          for (int j = 0; j < 4; ++j) r[j] = relu(acc[i][ct][j]);
+          u16x4 o = T::pack4(r);
           if (!keep) o = (u16x4)0;
           if (m < C2_PIX) *(u16x4*)(c2 + c2_wr[i] + ct * 2 * P2 * 8) = o;
         }
@@ -311,7 +316,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         for (int ct = 0; ct < 2; ++ct) {
           const f32x4 v = acc[i][ct];
           const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-          ostg[((wave * 4 + i) * 4 + g) * 40 + ct * 16 + r16] = T::from_f32(fmaxf(mx, 0.f));
+          ostg[((wave * 4 + i) * 4 + g) * 40 + ct * 16 + r16] = T::from_f32(relu(mx));
         }
     }
     __syncthreads();

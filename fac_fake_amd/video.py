@@ -1,0 +1,139 @@
+"""Config 3: one video through face crops -> CViT -> video score, on 1..N GPUs.
+
+The reference's ``predict`` (CViT-main/cvit_prediction.py:153-242) reads
+frames with cv2, finds faces with face_recognition (dlib HOG, CPU), crops and
+resizes them (``face_face_rec`` :106-121) and scores the crops.  Detection
+and video decoding stay outside this path ("only the
+crop/resize part is in scope, on synthetic boxes"), so a video here is a
+device tensor of decoded BGR frames plus one face box list per frame, and
+everything from the crop on runs on the GPU:
+
+* ``crop_faces``: ``frame[top:bottom, left:right]`` -> INTER_AREA resize to
+  224x224 -> BGR->RGB, all boxes in one ``fac_crop_resize_u8`` launch
+  (fac_fake_amd/csrc/crop.hip), uint8 straight into the conv stack's input
+  layout (the reference's float NCHW H2D copy and per-image Python
+  normalisation loop, :206-215, disappear: normalisation is fused into conv1).
+* ``mode="reference"``: the reference's frame schedule (``frame_indices``:
+  frames 0, 0, 5, 10, ... for int(0.1 * length) reads, :165-198), at most
+  5 faces per frame (:110) and 29 crops per video (:194), one chunk of slots
+  0..n-1; the video score as ``pre_process_prediction(pred_sig(.))``.
+* ``mode="dense"``: every box of every frame, crop j at pos slot j mod 32,
+  sharded contiguously over the ranks of ``group`` (one process per GPU); the
+  only collective is the all-gather of per-crop logits (``sharding``,
+  RCCL over xGMI with backend "nccl") before the score.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .prediction import EMPTY_SCORE, chunk_slots, dense_slots, pre_process_prediction, pred_sig
+from .sharding import gather_logits, shard_bounds
+from .weights import splitmix64
+
+CROP = 224
+FACES_PER_FRAME = 5          # cvit_prediction.py:110 (count < 5)
+MAX_CROPS_REFERENCE = 29     # cvit_prediction.py:194 (count_face_rec < 29)
+FRAME_JUMP = 5               # cvit_prediction.py:168
+
+
+def frame_indices(length: int) -> list[int]:
+    """Frames the reference reads: int(0.1 * length) iterations of read-then-seek
+    (cvit_prediction.py:165-198), i.e. 0, 0, 5, 10, ... (every read successful)."""
+    count = int(length * 0.1)
+    out, pos, start = [], 0, 0
+    for _ in range(count):
+        out.append(pos)
+        pos, start = start, start + FRAME_JUMP
+    return out
+
+
+def synthetic_video(n_frames: int, height: int = 1080, width: int = 1920, seed: int = 3, device=None,
+                    faces_per_frame: int = 1):
+    """Deterministic synthetic video: uint8 BGR frames [F, H, W, 3] on `device`
+    (torch's seeded device generator) and face boxes int32 [F*k, 5] =
+    (frame, left, top, right, bottom), square boxes of 240..559 px inside the
+    frame (splitmix64 of `seed`)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(seed)
+    frames = torch.randint(0, 256, (n_frames, height, width, 3), dtype=torch.uint8, device=dev, generator=g)
+    r = splitmix64(np.arange(3 * n_frames * faces_per_frame, dtype=np.uint64), seed + 1000).reshape(-1, 3)
+    size = 240 + (r[:, 0] % np.uint64(320)).astype(np.int64)
+    size = np.minimum(size, min(height, width))
+    left = (r[:, 1] % (np.uint64(width) - size.astype(np.uint64) + np.uint64(1))).astype(np.int64)
+    top = (r[:, 2] % (np.uint64(height) - size.astype(np.uint64) + np.uint64(1))).astype(np.int64)
+    f = np.repeat(np.arange(n_frames, dtype=np.int64), faces_per_frame)
+    boxes = np.stack([f, left, top, left + size, top + size], 1).astype(np.int32)
+    return frames, boxes
+
+
+def crop_faces(frames: torch.Tensor, boxes) -> torch.Tensor:
+    """uint8 BGR frames [F, H, W, 3] (device) + boxes [n, 5] -> uint8 RGB crops [n, 224, 224, 3] (device)."""
+    if not frames.is_cuda or frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
+        raise ValueError("frames must be a uint8 [F, H, W, 3] device tensor")
+    b = torch.as_tensor(np.asarray(boxes, dtype=np.int32).reshape(-1, 5)).to(frames.device)
+    n = int(b.shape[0])
+    crops = torch.empty(n, CROP, CROP, 3, dtype=torch.uint8, device=frames.device)
+    if n:
+        frames = frames.contiguous()
+        F, H, W, _ = frames.shape
+        lib = _lib.load()
+        _lib.check(lib.fac_crop_resize_u8(frames.data_ptr(), F, H, W, b.data_ptr(), n, crops.data_ptr(),
+                                          torch.cuda.current_stream(frames.device).cuda_stream),
+                   None, "fac_crop_resize_u8")
+    return crops
+
+
+def reference_boxes(boxes, length: int) -> np.ndarray:
+    """The boxes the reference would crop: per frame read (frame_indices), that
+    frame's first 5 faces, until 29 crops (cvit_prediction.py:107-121,189-196)."""
+    boxes = np.asarray(boxes, dtype=np.int32).reshape(-1, 5)
+    per_frame = {}
+    for bx in boxes:
+        per_frame.setdefault(int(bx[0]), []).append(bx)
+    out = []
+    for f in frame_indices(length):
+        for bx in per_frame.get(f, [])[:FACES_PER_FRAME]:
+            if len(out) < MAX_CROPS_REFERENCE:
+                out.append(bx)
+    return np.asarray(out, dtype=np.int32).reshape(-1, 5)
+
+
+def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", group=None,
+                  return_logits: bool = False):
+    """Video probability (< 0.5 REAL, >= 0.5 FAKE) of one video.
+
+    ``model``: fac_fake_amd.cvit.CViT (weights loaded, on this rank's GPU);
+    ``frames``: this rank's copy of the decoded video (device); ``boxes``:
+    [n, 5] (frame, left, top, right, bottom).  In dense mode with a process
+    group, every rank must call this with the same ``boxes``.
+    """
+    length = int(frames.shape[0])
+    if mode == "reference":
+        sel = reference_boxes(boxes, length)
+        if len(sel) == 0:
+            return (float(EMPTY_SCORE), None) if return_logits else float(EMPTY_SCORE)
+        crops = crop_faces(frames, sel)
+        with torch.no_grad():
+            logits = model.forward_u8(crops, pos_index=torch.from_numpy(chunk_slots(len(sel))))
+    elif mode == "dense":
+        boxes = np.asarray(boxes, dtype=np.int32).reshape(-1, 5)
+        n = len(boxes)
+        if n == 0:
+            return (float(EMPTY_SCORE), None) if return_logits else float(EMPTY_SCORE)
+        world = dist.get_world_size(group) if group is not None or dist.is_initialized() else 1
+        rank = dist.get_rank(group) if world > 1 else 0
+        lo, hi = shard_bounds(n, world, rank)
+        if hi > lo:
+            crops = crop_faces(frames, boxes[lo:hi])
+            with torch.no_grad():
+                local = model.forward_u8(crops, pos_index=torch.from_numpy(dense_slots(hi - lo, offset=lo)))
+        else:
+            local = torch.zeros(0, 2, dtype=torch.float32, device=frames.device)
+        logits = gather_logits(local.float(), n, group) if world > 1 else local
+    else:
+        raise ValueError("mode must be 'reference' or 'dense'")
+    score = float(pre_process_prediction(pred_sig(logits.float().cpu())))
+    return (score, logits) if return_logits else score

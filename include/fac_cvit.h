@@ -133,6 +133,16 @@ int fac_check_device_errors(fac_ctx* ctx, int* flags);
  * cvit_prediction.py:240,258-281): d_score = fp32 scalar. */
 int fac_video_score(const float* d_logits, int n, float* d_score, void* stream);
 
+/* Face crops of config 3 (cvit_prediction.py:111-116): for each box
+ * (frame, left, top, right, bottom) in d_boxes (int32 [n_boxes][5]), take
+ * frame[top:bottom, left:right] of the BGR uint8 frames [n_frames][H][W][3],
+ * area-resize it to 224x224 (cv2.INTER_AREA's area weights, evaluated in
+ * exact integer arithmetic, round half up) and swap BGR -> RGB (the
+ * cvtColor of :115) into d_crops [n_boxes][224][224][3]: the input of
+ * fac_forward_nhwc_u8.  Boxes are clipped to the frame; empty boxes give 0. */
+int fac_crop_resize_u8(const uint8_t* d_frames, int n_frames, int H, int W, const int32_t* d_boxes, int n_boxes,
+                       uint8_t* d_crops, void* stream);
+
 /* Tuning knob: run the conv stem in sub-batches of `crops` crops (0 = whole
  * batch), so intermediate activations stay resident in the Infinity Cache. */
 int fac_set_stem_chunk(fac_ctx* ctx, int crops);

@@ -425,3 +425,41 @@ def test_pipelined_forward_matches_synchronous(models):
                                        torch.cuda.current_stream().cuda_stream), None, "video_score")
         torch.cuda.synchronize()
         assert torch.equal(scores[i].cpu(), sc.cpu()), i
+
+
+def test_crop_resize_kernel_matches_oracle():
+    """fac_crop_resize_u8 (crop + INTER_AREA area weights in exact integers +
+    BGR->RGB) is bit-identical to oracle/video.py on downscales (odd and
+    even sizes), the 224 identity, upscales, boxes clipped by the frame,
+    empty boxes and out-of-range frame indices."""
+    from fac_fake_amd.video import crop_faces
+    from oracle import video as ov
+    rng = np.random.default_rng(11)
+    frames = rng.integers(0, 256, (5, 720, 1280, 3), dtype=np.uint8)
+    boxes = np.array([[0, 10, 20, 234, 244], [1, 100, 50, 551, 501], [2, 0, 0, 333, 257], [3, 1000, 400, 1280, 720],
+                      [4, 37, 41, 137, 141], [0, 1200, 600, 1500, 900], [1, -30, -40, 270, 260],
+                      [2, 5, 5, 5, 300], [9, 0, 0, 300, 300], [4, 640, 0, 641, 720], [3, 3, 7, 1279, 719]],
+                     np.int32)
+    got = crop_faces(torch.from_numpy(frames).to(DEV), boxes).cpu().numpy()
+    want = ov.crop_batch(frames, boxes)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("mode", ["reference", "dense"])
+def test_video_driver_matches_drop_in(models, mode):
+    """Config 3 on one GPU: predict_video's logits are bit-identical to the
+    drop-in CViT scoring the oracle's crops with the reference's slots, and
+    the score is the reference scoring rule applied to them."""
+    from fac_fake_amd.prediction import chunk_slots, dense_slots, pre_process_prediction, pred_sig
+    from fac_fake_amd.video import predict_video, reference_boxes, synthetic_video
+    from oracle import video as ov
+    m = models["bf16"]
+    frames, boxes = synthetic_video(60, 1080, 1920, seed=3, device=DEV)
+    score, logits = predict_video(m, frames, boxes, mode=mode, return_logits=True)
+    sel = reference_boxes(boxes, 60) if mode == "reference" else boxes
+    slots = chunk_slots(len(sel)) if mode == "reference" else dense_slots(len(sel))
+    crops = torch.from_numpy(ov.crop_batch(frames.cpu().numpy(), sel)).to(DEV)
+    ref = m.forward_u8(crops, pos_index=torch.from_numpy(slots)).cpu()
+    assert len(sel) == (6 if mode == "reference" else 60)
+    assert torch.equal(logits.cpu(), ref)
+    assert score == float(pre_process_prediction(pred_sig(ref)))
