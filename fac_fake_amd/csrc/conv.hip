@@ -79,7 +79,7 @@ __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, 
 // 1: it is loaded between chunks, exposed, which halves the halo LDS so that
 // OCC = 3 workgroups share a CU and hide each other's exposed loads — the
 // 112^2 layers, whose 1-2 chunks leave little to pipeline within a box).
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2>
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true>
 __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
@@ -199,8 +199,17 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   const int nsteps = nchunks * 9;
   issue_w(0, wsrc);
   issue_w(1, wsrc + WSL);
+  if constexpr (PB) issue_w(2, nsteps > 2 ? wsrc + 2 * WSL : wsrc);
   issue_halo(smem, 0);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  // PB: the B fragments of tap t+1 are read during tap t as well (slice s+1
+  // is retired one barrier earlier, slice s+3 is issued at step s into the
+  // slot slice s vacated when its fragments went to registers in step s-1).
+  u16x8 bcur[CTW];
+  if constexpr (PB) {
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) bcur[ct] = *(const u16x8*)(wring + bbase[ct]);
+  }
   // Software pipeline on the halo fragments: tap t multiplies pixel
   // fragments read during tap t-1 and, right behind each row tile's MFMAs,
   // reads that tile's fragment for tap t+1 (at t = 8: tap 0 of the next
@@ -210,6 +219,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   u16x8 fa[RTW];
 #pragma unroll
   for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(smem + abase[rt]);
+  // PB: slot 0 is re-filled at step 0, after every wave has read slice 0
+  if constexpr (PB) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   for (int c = 0; c < nchunks; ++c) {
     if constexpr (HB == 1) {
@@ -230,24 +241,44 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       // issue order: slice s+2, then (t = 0) the next chunk's halo into the
       // other halo buffer (on the last chunk a dummy re-read of this chunk);
       // glds are LDS writes, so the compiler keeps them in program order
-      issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
+      if constexpr (PB)
+        issue_w(t % 3, (c * 9 + t + 3 < nsteps) ? wnext + (t + 1) * WSL : wsrc);
+      else
+        issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
       if (HB == 2 && t == 0) issue_halo(smem + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
-      const uint16_t* wb = wring + (t % 3) * WSL;
-      u16x8 bfr[CTW];
+      u16x8 bfr[CTW], bnx[CTW];
+      if constexpr (PB) {
 #pragma unroll
-      for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
+        for (int ct = 0; ct < CTW; ++ct) bfr[ct] = bcur[ct];
+      } else {
+        const uint16_t* wb = wring + (t % 3) * WSL;
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
+      }
       constexpr int ntoff = t < 8 ? (((t + 1) / 3) * HALO_RP + ((t + 1) % 3)) * 8 : 0;
       const uint16_t* hnx = t < 8 ? hb : hbn;
+      const uint16_t* wbn = wring + ((t + 1) % 3) * WSL;
 #pragma unroll
       for (int rt = 0; rt < RTW; ++rt) {
 #pragma unroll
         for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
         // (HB = 1: the next chunk's tap-0 fragments are read once its halo is in)
         if (HB == 2 || t < 8) fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, CTW, 0);
+        if (PB && rt == 0) {
 #pragma unroll
-      for (int rt = 0; rt < RTW; ++rt) {
+          for (int ct = 0; ct < CTW; ++ct) bnx[ct] = *(const u16x8*)(wbn + bbase[ct]);
+        }
+      }
+      if constexpr (PB) {
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) bcur[ct] = bnx[ct];
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x100, CTW, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, PB ? 1 + CTW : 1, 0);
+#pragma unroll
+      for (int rt = 1; rt < RTW; ++rt) {
         __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
@@ -425,15 +456,15 @@ int conv_block_n(int H) {
   }
 }
 
-template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2>
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true>
 static void launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                        int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if (pool)
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC>
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
         <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
   else
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC>
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
         <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
 }
 
@@ -442,13 +473,13 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
                                 int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st) {
   if (W != H) return hipErrorInvalidValue;
   switch (H) {
-    case 224: launch_box<T, 16, 16, 32, 4, 1>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 224: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
     // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
-    case 112: launch_box<T, 16, 16, 64, 4, 1, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 112: launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
-    case 14: launch_box<T, 14, 14, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 14: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

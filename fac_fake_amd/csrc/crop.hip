@@ -10,7 +10,7 @@
 // [224 s, 224 s + 224), so every weight is an exact integer overlap ov and
 //   out = round( sum_y sum_x ov_y ov_x src / (n_x n_y) )      (round half up)
 // in integer arithmetic: the GPU kernel and the numpy restatement
-// (oracle/crop_area.py) agree bit for bit.  cv2 itself evaluates the same
+// (oracle/video.py) agree bit for bit.  cv2 itself evaluates the same
 // sum with float weights, so it may differ by one count on exact .5 ties
 // (cv2 is not in the image: parity with it is unpinned).
 // Boxes are clipped to the frame; an empty box gives a zero crop.
