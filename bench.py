@@ -79,6 +79,42 @@ def cpu_baseline(sd, threads: int, iters: int = 4, batch: int = 32):
                       f"1 warm-up), torch {torch.__version__}"}
 
 
+def video_measurement(model, dev, world: int, n_frames: int = 300, reps: int = 3):
+    """Config 3 (BASELINE.json configs[2]): one synthetic 300-frame 1080x1920
+    BGR video resident in HBM with one face box per frame -> GPU crop +
+    INTER_AREA resize + BGR->RGB -> CViT -> video score, dense mode (every
+    frame's crop, slot j mod 32), crops sharded over the ranks with one RCCL
+    all-gather of logits (fac_fake_amd/video.py).  Also the reference-mode
+    call (the reference's frame schedule: <= 29 crops).  Timed end to end
+    (host-synchronised, max over ranks), so it includes the launch and the
+    score's device->host read like cvit_prediction.py:242."""
+    from fac_fake_amd import video
+    frames, boxes = video.synthetic_video(n_frames, 1080, 1920, seed=3, device=dev)
+    out = {"workload": f"config 3: {n_frames}-frame 1080x1920 synthetic video, 1 box/frame, crop+resize+CViT+score",
+           "n_gpus": world}
+    for mode in ("dense", "reference"):
+        video.predict_video(model, frames, boxes, mode=mode)  # warm-up
+        torch.cuda.synchronize(dev)
+        ts = []
+        for _ in range(reps):
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            score = video.predict_video(model, frames, boxes, mode=mode)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        el = float(np.median(ts))
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        n = n_frames if mode == "dense" else len(video.reference_boxes(boxes, n_frames))
+        out[mode] = {"crops": n, "video_ms": round(el * 1e3, 3), "crops_per_s": round(n / el, 1),
+                     "score": round(float(score), 6)}
+    del frames
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,6 +129,7 @@ def main():
                          "that overlaps batch k's encoder with batch k+1's conv stack")
     ap.add_argument("--no-fuse", action="store_true", help="unfused conv1..conv3 (A/B of the fused 224 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-video", action="store_true", help="skip the config-3 video sub-measurement")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="fac_set_option knob (include/fac_cvit.h), repeatable")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
@@ -268,6 +305,8 @@ def main():
                      "launch_ms": round(float(conv_ms[dom]), 4), "flops_per_launch": dom_flops},
         "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, acc)},
     }
+    if not args.no_video:
+        line["config3"] = video_measurement(model, dev, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(sd, threads)

@@ -91,6 +91,7 @@ struct fac_ctx {
   int device = 0;
   int dtype = 0;
   bool loaded = false;
+  bool tail_only = false;  // option "tail_only": load/run only patch embedding .. head (ResVitKan)
   std::string err;
   std::vector<void*> weights;  // all weight allocations
   uint16_t* conv1_w = nullptr;
@@ -293,7 +294,7 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
 
   // ---- conv stem with BN folded
   int H = kImg;
-  for (int i = 0; i < 17; ++i) {
+  for (int i = 0; i < 17 && !c->tail_only; ++i) {
     const int ci = kStem[i][0], co = kStem[i][1];
     int cidx, bidx;
     stem_indices(i, &cidx, &bidx);
@@ -411,7 +412,7 @@ struct Prof {
 };
 
 int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, float* logits, float* probs,
-              hipStream_t st, Prof* prof);
+              hipStream_t st, Prof* prof, float* hidden_out = nullptr);
 
 // The synchronous forward on `stream`: conv stack -> stem_dst (default the
 // context's stem buffer 0), then (unless conv_only) the encoder and head.
@@ -421,6 +422,8 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   using namespace fac;
   if (!c) return FAC_ERR_ARG;
   if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "forward before fac_load_weights");
+  if (c->tail_only && !stem_in)
+    return set_err(c, FAC_ERR_NOT_LOADED, "tail-only context has no conv stem: use fac_forward_features");
   if (B <= 0 || (!in && !stem_in) || (stop_after < 0 && !conv_only && (!pidx || !logits)))
     return set_err(c, FAC_ERR_ARG, "bad forward arguments");
   DevGuard g(c->device);
@@ -524,7 +527,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
 // Patch embedding, the 6 encoder layers and the head on `st`, from the conv
 // stack's output `stem` [B,7,7,512] (cvit.py:171-179).
 int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, float* logits, float* probs,
-              hipStream_t st, Prof* prof) {
+              hipStream_t st, Prof* prof, float* hidden_out) {
   using namespace fac;
   const int dt = c->dtype;
 #define MARK(sid)                                  \
@@ -566,9 +569,11 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
   }
   MARK(18);
   HIP_TRY(c, launch_resid_cls(dt, c->x, c->slab, SK, c->tl[kDepth - 1].b2, c->cbuf, B, st));
-  HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, c->hh, kMlp, B, kMlp, kDim, 1, st,
+  // hidden_out: the ReLU'd first head layer is the result (ResVitKan's KAN head follows)
+  float* hh = hidden_out ? hidden_out : c->hh;
+  HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, hh, kMlp, B, kMlp, kDim, 1, st,
                          c->gemm_var[5]));
-  HIP_TRY(c, launch_head_out(c->hh, c->h2_w, c->h2_b, logits, probs, B, st));
+  if (logits) HIP_TRY(c, launch_head_out(hh, c->h2_w, c->h2_b, logits, probs, B, st));
   MARK(19);
 #undef MARK
   return FAC_OK;
@@ -631,6 +636,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (!c || !key) return FAC_ERR_ARG;
   const std::string k(key);
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
+  if (k == "tail_only") {
+    if (c->loaded) return set_err(c, FAC_ERR_ARG, "tail_only must be set before fac_load_weights");
+    c->tail_only = value != 0;
+    return FAC_OK;
+  }
   if (k == "fuse_stem224") {
     c->fuse_stem224 = value != 0;
     return FAC_OK;
@@ -653,6 +663,22 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     return FAC_OK;
   }
   return set_err(c, FAC_ERR_ARG, "unknown option " + k);
+}
+
+int fac_forward_features(fac_ctx* c, const void* d_feat, int B, const int32_t* d_pos, float* d_hidden,
+                         float* d_logits, float* d_probs, void* stream) {
+  if (!c) return FAC_ERR_ARG;
+  if (!c->loaded) return set_err(c, FAC_ERR_NOT_LOADED, "forward before fac_load_weights");
+  if (!d_feat || !d_pos || B <= 0 || (!d_hidden && !d_logits))
+    return set_err(c, FAC_ERR_ARG, "bad fac_forward_features arguments");
+  if (B > 32 * 1024) return set_err(c, FAC_ERR_SHAPE, "batch too large");
+  DevGuard g(c->device);
+  int rc = ensure_ws(c, B);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  for (int i = 0; i < 2; ++i)
+    if (c->tail_pending[i]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[i], 0));
+  return tail_impl(c, (const uint16_t*)d_feat, B, d_pos, d_logits, d_probs, st, nullptr, d_hidden);
 }
 
 int fac_forward_nchw_f32(fac_ctx* c, const float* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,

@@ -1,0 +1,515 @@
+// Layer-level kernels for the §8f model families (include/fac_ops.h):
+//   * convnd_igemm: N-d convolution + folded BN (+ ReLU, + residual) as an
+//     implicit GEMM on MFMA — the ResNet-50 stem of ResVitKan
+//     (CViT-main/ResVitKan/ResVitKan.py:124-240) and S3D's Conv3d layers
+//     (sx_exp_deepfakedetect-master/S3D/model.py:50-82);
+//   * pool_nd: max / average pooling, channels-last;
+//   * pack_input: 3-channel image staging (uint8 or fp32 planar -> 16-bit);
+//   * KANLinear (CViT-main/ResVitKan/kan.py:90-132, 189-206) in fp32.
+//
+// convnd_igemm: rows = output positions, columns = output channels,
+// k = (tap, 8-channel piece).  A 128 x BN output tile per 256-thread
+// workgroup (4 waves, 2 x 2, each 64 x BN/2 = 4 x BN/32 MFMA tiles), K in
+// steps of 32 (4 pieces of 8 channels).  The A tile is gathered on the fly
+// (im2col-free): every thread owns one GEMM row and two of its four pieces,
+// tracks its pieces' (channel piece, tap) incrementally (no divisions in the
+// K loop) and loads 16 bytes per piece, zero outside the input (padding) or
+// beyond the real K.  Operands are register-staged into a double-buffered LDS
+// image [piece][row] (16-byte entries: the 16 lanes of a ds_read_b128 group
+// read 16 consecutive entries, conflict-free), one barrier per K step, the
+// next step's global loads in flight during the current step's MFMAs.  The
+// epilogue stages the fp32 tile in LDS and writes 16-byte channel vectors
+// (bias, ReLU, residual, ReLU, convert), so a row's BN channels leave in one
+// contiguous burst.
+#include "common.hpp"
+#include "fac_cvit.h"
+#include "fac_ops.h"
+
+namespace fac {
+
+struct ConvP {
+  const uint16_t* in;
+  const uint16_t* w;
+  const float* bias;
+  const uint16_t* res;
+  void* out;
+  int D, H, W, C8;
+  int Do, Ho, Wo, Cout;
+  int KD, KH, KW;
+  int SD, SH, SW, PD, PH, PW;
+  int Kp, ksteps, ktot8;
+  int ldo, c_off, ldr, r_off, flags;
+  int vec_out, vec_res;
+  int M;
+};
+
+// (channel piece, tap) of one K piece, advanced in place by 4 pieces
+struct Trk {
+  int c8, tx, ty, tz, kp;
+};
+
+__device__ __forceinline__ void trk_norm(Trk& t, int C8, int KH, int KW) {
+  while (t.c8 >= C8) {
+    t.c8 -= C8;
+    if (++t.tx == KW) {
+      t.tx = 0;
+      if (++t.ty == KH) {
+        t.ty = 0;
+        ++t.tz;
+      }
+    }
+  }
+}
+
+template <class T, int BN>
+__global__ __launch_bounds__(256, 2) void convnd_igemm(ConvP p) {
+  constexpr int BM = 128;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int RT = WTM / 16, CT = WTN / 16;
+  constexpr int NBP = BN * 4 / 256;           // B pieces per thread per K step
+  constexpr int SPITCH = BN + 4;              // fp32 staging row pitch
+  constexpr int OPER = 2 * (4 * BM + 4 * BN) * 8;  // u16 elements, double-buffered
+  constexpr int STG = BM * SPITCH * 2;        // u16 elements of the fp32 staging tile
+  constexpr int SMEM = OPER > STG ? OPER : STG;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+  uint16_t* const sA = smem;                  // [2][4][BM][8]
+  uint16_t* const sB = smem + 2 * 4 * BM * 8;  // [2][4][BN][8]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  int bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);  // XCD-contiguous row tiles
+  const int m0 = bx * BM, n0 = blockIdx.y * BN;
+
+  // ---- A gather state: one row, pieces ja and ja + 2 of every K step
+  const int arow = tid & (BM - 1), ja = tid >> 7;
+  const int m = m0 + arow;
+  const bool mvalid = m < p.M;
+  int iz0, iy0, ix0;
+  const uint16_t* inb;
+  {
+    const int mm = mvalid ? m : 0;
+    const int ox = mm % p.Wo, t1 = mm / p.Wo;
+    const int oy = t1 % p.Ho, t2 = t1 / p.Ho;
+    const int oz = t2 % p.Do, n = t2 / p.Do;
+    iz0 = oz * p.SD - p.PD;
+    iy0 = oy * p.SH - p.PH;
+    ix0 = ox * p.SW - p.PW;
+    inb = p.in + (size_t)n * p.D * p.H * p.W * p.C8 * 8;
+  }
+  Trk ta{ja, 0, 0, 0, ja}, tb{ja + 2, 0, 0, 0, ja + 2};
+  trk_norm(ta, p.C8, p.KH, p.KW);
+  trk_norm(tb, p.C8, p.KH, p.KW);
+  auto gather = [&](const Trk& t) -> u16x8 {
+    const int iz = iz0 + t.tz, iy = iy0 + t.ty, ix = ix0 + t.tx;
+    if (mvalid && t.kp < p.ktot8 && (unsigned)iz < (unsigned)p.D && (unsigned)iy < (unsigned)p.H &&
+        (unsigned)ix < (unsigned)p.W)
+      return *(const u16x8*)(inb + (((size_t)iz * p.H + iy) * p.W + ix) * p.C8 * 8 + t.c8 * 8);
+    return (u16x8)0;
+  };
+  auto advance = [&](Trk& t) {
+    t.kp += 4;
+    t.c8 += 4;
+    trk_norm(t, p.C8, p.KH, p.KW);
+  };
+  // ---- B (weights [cout_pad][Kp]): row brow, piece jb (+2 for BN = 128)
+  const int brow = tid % BN, jb = tid / BN;
+  const uint16_t* wrow = p.w + (size_t)(n0 + brow) * p.Kp;
+
+  u16x8 ra0, ra1, rb[NBP];
+  auto load_step = [&](int s) {
+    ra0 = gather(ta);
+    ra1 = gather(tb);
+#pragma unroll
+    for (int i = 0; i < NBP; ++i) rb[i] = *(const u16x8*)(wrow + (size_t)(s * 4 + jb + i * (256 / BN)) * 8);
+  };
+  auto store_step = [&](int buf) {
+    uint16_t* a = sA + buf * 4 * BM * 8;
+    uint16_t* b = sB + buf * 4 * BN * 8;
+    *(u16x8*)(a + (ja * BM + arow) * 8) = ra0;
+    *(u16x8*)(a + ((ja + 2) * BM + arow) * 8) = ra1;
+#pragma unroll
+    for (int i = 0; i < NBP; ++i) *(u16x8*)(b + ((jb + i * (256 / BN)) * BN + brow) * 8) = rb[i];
+  };
+
+  f32x4 acc[RT][CT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = (f32x4)0.f;
+
+  load_step(0);
+  store_step(0);
+  __syncthreads();
+  for (int s = 0; s < p.ksteps; ++s) {
+    const bool more = s + 1 < p.ksteps;
+    if (more) {
+      advance(ta);
+      advance(tb);
+      load_step(s + 1);
+    }
+    const uint16_t* a = sA + (s & 1) * 4 * BM * 8;
+    const uint16_t* b = sB + (s & 1) * 4 * BN * 8;
+    u16x8 fb[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) fb[ct] = *(const u16x8*)(b + ((lane >> 4) * BN + wn * WTN + ct * 16 + (lane & 15)) * 8);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const u16x8 fa = *(const u16x8*)(a + ((lane >> 4) * BM + wm * WTM + rt * 16 + (lane & 15)) * 8);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = T::mfma(fa, fb[ct], acc[rt][ct]);
+    }
+    if (more) store_step((s + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias (+ReLU) in registers -> fp32 LDS tile -> 8-channel vectors
+  float* stg = (float*)smem;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = wn * WTN + ct * 16 + (lane & 15);
+    const float bv = p.bias ? p.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[rt][ct][r] + bv;
+        if (p.flags & FAC_CONV_RELU) v = relu(v);
+        stg[(wm * WTM + rt * 16 + (lane >> 4) * 4 + r) * SPITCH + col] = v;
+      }
+  }
+  __syncthreads();
+  constexpr int QPR = BN / 8;  // 8-channel pieces per row
+#pragma unroll 2
+  for (int q = tid; q < BM * QPR; q += 256) {
+    const int row = q / QPR, cp = q - row * QPR;
+    const int mo = m0 + row, c = n0 + cp * 8;
+    if (mo >= p.M || c >= p.Cout) continue;
+    const int nc = min(8, p.Cout - c);
+    const f32x4 lo = *(const f32x4*)(stg + row * SPITCH + cp * 8);
+    const f32x4 hi = *(const f32x4*)(stg + row * SPITCH + cp * 8 + 4);
+    float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (p.flags & FAC_CONV_RESID) {
+      const uint16_t* r = p.res + (size_t)mo * p.ldr + p.r_off + c;
+      if (p.vec_res && nc == 8) {
+        const u16x8 rv = *(const u16x8*)r;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += T::to_f32(rv[i]);
+      } else {
+        for (int i = 0; i < nc; ++i) v[i] += T::to_f32(r[i]);
+      }
+    }
+    if (p.flags & FAC_CONV_RELU2) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = relu(v[i]);
+    }
+    if (p.flags & FAC_CONV_OUT_F32) {
+      float* o = (float*)p.out + (size_t)mo * p.ldo + p.c_off + c;
+      for (int i = 0; i < nc; ++i) o[i] = v[i];
+    } else {
+      uint16_t* o = (uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c;
+      if (p.vec_out && nc == 8) {
+        const u16x4 a = T::pack4((f32x4){v[0], v[1], v[2], v[3]});
+        const u16x4 b = T::pack4((f32x4){v[4], v[5], v[6], v[7]});
+        *(u16x8*)o = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+      } else {
+        for (int i = 0; i < nc; ++i) o[i] = T::from_f32(v[i]);
+      }
+    }
+  }
+}
+
+// ---- pooling: one thread per (output position, 8-channel piece)
+template <class T>
+__global__ __launch_bounds__(256) void pool_nd(fac_pool_desc p, int total) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int C8 = p.c / 8;
+  const int c8 = t % C8, mo = t / C8;
+  const int ox = mo % p.ow, t1 = mo / p.ow;
+  const int oy = t1 % p.oh, t2 = t1 / p.oh;
+  const int oz = t2 % p.od, n = t2 / p.od;
+  const uint16_t* inb = (const uint16_t*)p.in + (size_t)n * p.d * p.h * p.w * p.c + c8 * 8;
+  float a[8];
+  const bool mx = p.mode == 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = mx ? -__builtin_inff() : 0.f;
+  for (int kz = 0; kz < p.kd; ++kz) {
+    const int iz = oz * p.sd - p.pd + kz;
+    if ((unsigned)iz >= (unsigned)p.d) continue;
+    for (int ky = 0; ky < p.kh; ++ky) {
+      const int iy = oy * p.sh - p.ph + ky;
+      if ((unsigned)iy >= (unsigned)p.h) continue;
+      for (int kx = 0; kx < p.kw; ++kx) {
+        const int ix = ox * p.sw - p.pw + kx;
+        if ((unsigned)ix >= (unsigned)p.w) continue;
+        const u16x8 v = *(const u16x8*)(inb + (((size_t)iz * p.h + iy) * p.w + ix) * p.c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float f = T::to_f32(v[i]);
+          a[i] = mx ? fmaxf(a[i], f) : a[i] + f;
+        }
+      }
+    }
+  }
+  if (!mx) {
+    const float inv = (float)(p.kd * p.kh * p.kw);  // count_include_pad=True
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = a[i] / inv;
+  }
+  const u16x4 lo = T::pack4((f32x4){a[0], a[1], a[2], a[3]});
+  const u16x4 hi = T::pack4((f32x4){a[4], a[5], a[6], a[7]});
+  *(u16x8*)((uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c8 * 8) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// ---- input staging
+template <class T, bool U8>
+__global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
+                                                  float m2, float s0, float s1, float s2, uint16_t* out, int c_pad) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)n_img * S) return;
+  const int n = (int)(t / S), s = (int)(t - (long long)n * S);
+  float x[3];
+  if constexpr (U8) {
+    const uint8_t* p = (const uint8_t*)src + (size_t)t * 3;
+    x[0] = (float)p[0];
+    x[1] = (float)p[1];
+    x[2] = (float)p[2];
+  } else {
+    const float* p = (const float*)src + (size_t)n * 3 * S + s;
+    x[0] = p[0];
+    x[1] = p[(size_t)S];
+    x[2] = p[(size_t)2 * S];
+  }
+  const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
+  uint16_t* o = out + (size_t)t * c_pad;
+  u16x8 v = (u16x8)0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) v[c] = T::from_f32((x[c] / div - mean[c]) / sd[c]);
+  *(u16x8*)o = v;
+  for (int c = 8; c < c_pad; c += 8) *(u16x8*)(o + c) = (u16x8)0;
+}
+
+// ---- KANLinear
+// Cox-de Boor recursion of kan.py:90-132 for one input value, in the
+// reference's operation order (no contraction: the file is compiled with
+// -ffp-contract=off semantics via the explicit _rn intrinsics).
+template <int NK>
+__device__ __forceinline__ void kan_bases(float x, const float* g, float* b) {
+  constexpr int NB0 = NK - 1;
+#pragma unroll
+  for (int j = 0; j < NB0; ++j) b[j] = (x >= g[j] && x < g[j + 1]) ? 1.f : 0.f;
+#pragma unroll
+  for (int k = 1; k <= 3; ++k) {
+#pragma unroll
+    for (int j = 0; j < NB0 - k; ++j) {
+      const float l = __fmul_rn(__fdiv_rn(__fsub_rn(x, g[j]), __fsub_rn(g[j + k], g[j])), b[j]);
+      const float r = __fmul_rn(__fdiv_rn(__fsub_rn(g[j + k + 1], x), __fsub_rn(g[j + k + 1], g[j + 1])), b[j + 1]);
+      b[j] = __fadd_rn(l, r);
+    }
+  }
+}
+
+constexpr int kKanNK = 12;             // grid_size 5 + 2*order 3 + 1 knots
+constexpr int kKanF = 1 + kKanNK - 4;  // silu + 8 bases per input
+constexpr int kKanRows = 32, kKanIn = 32;
+
+// grid (in-chunks, row-chunks): features of 32 rows x 32 inputs into LDS,
+// then every (row, out) pair of the chunk accumulates its 32 x 9 products
+// into a partial slab [in-chunk][row][out] (summed in chunk order after).
+__global__ __launch_bounds__(256) void kan_partial(const float* __restrict__ x, int rows, int in_f, int out_f,
+                                                   const float* __restrict__ grid, const float* __restrict__ wcat,
+                                                   float* __restrict__ part) {
+  __shared__ float feat[kKanRows][kKanIn * kKanF + 1];
+  const int ic = blockIdx.x, r0 = blockIdx.y * kKanRows, i0 = ic * kKanIn;
+  const int ni = min(kKanIn, in_f - i0), nr = min(kKanRows, rows - r0);
+  for (int t = threadIdx.x; t < kKanRows * kKanIn; t += 256) {
+    const int r = t / kKanIn, i = t - r * kKanIn;
+    float* f = &feat[r][i * kKanF];
+    if (r < nr && i < ni) {
+      const float v = x[(size_t)(r0 + r) * in_f + i0 + i];
+      f[0] = v / (1.f + expf(-v));  // SiLU
+      float g[kKanNK], b[kKanNK - 1];
+#pragma unroll
+      for (int k = 0; k < kKanNK; ++k) g[k] = grid[(size_t)(i0 + i) * kKanNK + k];
+      kan_bases<kKanNK>(v, g, b);
+#pragma unroll
+      for (int k = 0; k < kKanF - 1; ++k) f[1 + k] = b[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < kKanF; ++k) f[k] = 0.f;
+    }
+  }
+  __syncthreads();
+  const int K = ni * kKanF;
+  for (int q = threadIdx.x; q < nr * out_f; q += 256) {
+    const int r = q / out_f, o = q - r * out_f;
+    const float* w = wcat + ((size_t)o * in_f + i0) * kKanF;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = fmaf(feat[r][k], w[k], acc);
+    part[((size_t)ic * rows + r0 + r) * out_f + o] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void kan_reduce(const float* __restrict__ part, int chunks, int n, float* __restrict__ y) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  float s = 0.f;
+  for (int c = 0; c < chunks; ++c) s += part[(size_t)c * n + t];
+  y[t] = s;
+}
+
+__global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, float* __restrict__ y, int n) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t < n) y[t] = 1.f / (1.f + expf(-x[t]));
+}
+
+template <class T>
+static hipError_t launch_convnd(const ConvP& p, int cout_pad, hipStream_t st) {
+  const int gx = (p.M + 127) / 128;
+  if (cout_pad % 128 == 0 && p.Cout > 64) {
+    convnd_igemm<T, 128><<<dim3(gx, cout_pad / 128), 256, 0, st>>>(p);
+  } else {
+    convnd_igemm<T, 64><<<dim3(gx, (p.Cout + 63) / 64), 256, 0, st>>>(p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fac
+
+extern "C" {
+
+int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad) {
+  if (cout <= 0 || cin <= 0 || kd <= 0 || kh <= 0 || kw <= 0 || !cout_pad || !k_pad) return FAC_ERR_ARG;
+  *cout_pad = (cout + 127) / 128 * 128;
+  *k_pad = (kd * kh * kw * cin + 31) / 32 * 32;
+  return FAC_OK;
+}
+
+int fac_conv_nd(const fac_conv_desc* d, void* stream) {
+  using namespace fac;
+  if (!d || !d->in || !d->weight || !d->out) return FAC_ERR_ARG;
+  if (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16) return FAC_ERR_ARG;
+  if (d->cin <= 0 || d->cin % 8 || d->cout <= 0 || d->n <= 0 || d->d <= 0 || d->h <= 0 || d->w <= 0) return FAC_ERR_SHAPE;
+  if (d->kd <= 0 || d->kh <= 0 || d->kw <= 0 || d->sd <= 0 || d->sh <= 0 || d->sw <= 0) return FAC_ERR_SHAPE;
+  if (d->pd < 0 || d->ph < 0 || d->pw < 0 || d->od <= 0 || d->oh <= 0 || d->ow <= 0) return FAC_ERR_SHAPE;
+  // output dims must be the floor-mode ones (every gathered tap then stays
+  // within the padded input)
+  if (d->od != (d->d + 2 * d->pd - d->kd) / d->sd + 1 || d->oh != (d->h + 2 * d->ph - d->kh) / d->sh + 1 ||
+      d->ow != (d->w + 2 * d->pw - d->kw) / d->sw + 1)
+    return FAC_ERR_SHAPE;
+  int cout_pad, k_pad;
+  fac_conv_weight_layout(d->cout, d->cin, d->kd, d->kh, d->kw, &cout_pad, &k_pad);
+  if (d->k_pad != k_pad) return FAC_ERR_SHAPE;
+  if (d->ldo < d->c_off + d->cout || d->c_off < 0) return FAC_ERR_SHAPE;
+  if ((d->flags & FAC_CONV_RESID) && (!d->residual || d->ldr < d->r_off + d->cout || d->r_off < 0)) return FAC_ERR_ARG;
+  const long long M = (long long)d->n * d->od * d->oh * d->ow;
+  if (M >= (1LL << 31) || (long long)d->n * d->d * d->h * d->w * d->cin >= (1LL << 40)) return FAC_ERR_SHAPE;
+  ConvP p;
+  p.in = (const uint16_t*)d->in;
+  p.w = (const uint16_t*)d->weight;
+  p.bias = d->bias;
+  p.res = (const uint16_t*)d->residual;
+  p.out = d->out;
+  p.D = d->d;
+  p.H = d->h;
+  p.W = d->w;
+  p.C8 = d->cin / 8;
+  p.Do = d->od;
+  p.Ho = d->oh;
+  p.Wo = d->ow;
+  p.Cout = d->cout;
+  p.KD = d->kd;
+  p.KH = d->kh;
+  p.KW = d->kw;
+  p.SD = d->sd;
+  p.SH = d->sh;
+  p.SW = d->sw;
+  p.PD = d->pd;
+  p.PH = d->ph;
+  p.PW = d->pw;
+  p.Kp = k_pad;
+  p.ksteps = k_pad / 32;
+  p.ktot8 = d->kd * d->kh * d->kw * (d->cin / 8);
+  p.ldo = d->ldo;
+  p.c_off = d->c_off;
+  p.ldr = d->ldr;
+  p.r_off = d->r_off;
+  p.flags = d->flags;
+  p.vec_out = (d->ldo % 8 == 0 && d->c_off % 8 == 0) ? 1 : 0;
+  p.vec_res = (d->ldr % 8 == 0 && d->r_off % 8 == 0) ? 1 : 0;
+  p.M = (int)M;
+  hipStream_t st = (hipStream_t)stream;
+  const hipError_t e = d->dtype == FAC_DTYPE_BF16 ? launch_convnd<BF16>(p, cout_pad, st) : launch_convnd<F16>(p, cout_pad, st);
+  return e == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_pool_nd(const fac_pool_desc* d, void* stream) {
+  using namespace fac;
+  if (!d || !d->in || !d->out) return FAC_ERR_ARG;
+  if (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16) return FAC_ERR_ARG;
+  if (d->c <= 0 || d->c % 8 || d->n <= 0 || d->od <= 0 || d->oh <= 0 || d->ow <= 0 || d->mode < 0 || d->mode > 1)
+    return FAC_ERR_SHAPE;
+  if (d->kd <= 0 || d->kh <= 0 || d->kw <= 0 || d->sd <= 0 || d->sh <= 0 || d->sw <= 0) return FAC_ERR_SHAPE;
+  if (d->ldo % 8 || d->c_off % 8 || d->ldo < d->c_off + d->c) return FAC_ERR_SHAPE;
+  const long long total = (long long)d->n * d->od * d->oh * d->ow * (d->c / 8);
+  if (total >= (1LL << 31)) return FAC_ERR_SHAPE;
+  const int nb = (int)((total + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == FAC_DTYPE_BF16)
+    pool_nd<BF16><<<nb, 256, 0, st>>>(*d, (int)total);
+  else
+    pool_nd<F16><<<nb, 256, 0, st>>>(*d, (int)total);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_pack_input(int dtype, const void* src, int src_kind, int n, int s, float div, const float* mean3,
+                   const float* std3, void* out, int c_pad, void* stream) {
+  using namespace fac;
+  if (!src || !out || n <= 0 || s <= 0 || c_pad < 8 || c_pad % 8 || (src_kind != 0 && src_kind != 1) || !(div > 0.f))
+    return FAC_ERR_ARG;
+  if (dtype != FAC_DTYPE_BF16 && dtype != FAC_DTYPE_F16) return FAC_ERR_ARG;
+  const float m[3] = {mean3 ? mean3[0] : 0.f, mean3 ? mean3[1] : 0.f, mean3 ? mean3[2] : 0.f};
+  const float sd[3] = {std3 ? std3[0] : 1.f, std3 ? std3[1] : 1.f, std3 ? std3[2] : 1.f};
+  const long long total = (long long)n * s;
+  const int nb = (int)((total + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  uint16_t* o = (uint16_t*)out;
+#define FAC_PACK(TT, U)                                                                                      \
+  pack_input<TT, U><<<nb, 256, 0, st>>>(src, n, s, div, m[0], m[1], m[2], sd[0], sd[1], sd[2], o, c_pad)
+  if (dtype == FAC_DTYPE_BF16) {
+    if (src_kind == 0) FAC_PACK(BF16, true); else FAC_PACK(BF16, false);
+  } else {
+    if (src_kind == 0) FAC_PACK(F16, true); else FAC_PACK(F16, false);
+  }
+#undef FAC_PACK
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+size_t fac_kan_scratch_bytes(int rows, int in_f, int out_f) {
+  if (rows <= 0 || in_f <= 0 || out_f <= 0) return 0;
+  const size_t chunks = (in_f + fac::kKanIn - 1) / fac::kKanIn;
+  return chunks * rows * out_f * sizeof(float);
+}
+
+int fac_kan_linear(const float* x, int rows, int in_f, int out_f, const float* grid, int n_knots, const float* wcat,
+                   float* y, void* partial, void* stream) {
+  using namespace fac;
+  if (!x || !grid || !wcat || !y || !partial || rows <= 0 || in_f <= 0 || out_f <= 0) return FAC_ERR_ARG;
+  if (n_knots != kKanNK) return FAC_ERR_SHAPE;  // grid_size 5, spline_order 3 (kan.py:21-22)
+  const int chunks = (in_f + kKanIn - 1) / kKanIn;
+  hipStream_t st = (hipStream_t)stream;
+  kan_partial<<<dim3(chunks, (rows + kKanRows - 1) / kKanRows), 256, 0, st>>>(x, rows, in_f, out_f, grid, wcat,
+                                                                              (float*)partial);
+  const int n = rows * out_f;
+  kan_reduce<<<(n + 255) / 256, 256, 0, st>>>((const float*)partial, chunks, n, y);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_sigmoid(const float* x, float* y, int n, void* stream) {
+  if (!x || !y || n <= 0) return FAC_ERR_ARG;
+  fac::sigmoid_k<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(x, y, n);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,239 @@
+"""Layer-level gfx950 kernels (include/fac_ops.h) on torch device tensors.
+
+The §8f model families (ResVitKan, S3D) are sequences of ordinary layers:
+their Python mirrors fold BatchNorm and pack weights once here, then call one
+kernel per layer on the current torch stream (capturable into a hipGraph).
+Activations are 16-bit channels-last tensors shaped ``[N, D, H, W, C]``
+(``D = 1`` for 2-D nets), ``C`` a multiple of 8.  There is no CPU fallback:
+every call goes through ``libfac_cvit.so`` and raises if it cannot.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+
+TORCH16 = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
+RELU, RESID, RELU2, OUT_F32 = 1, 2, 4, 8   # FAC_CONV_* epilogue flags
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int), ("inp", ctypes.c_void_p),
+                ("n", ctypes.c_int), ("d", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
+                ("cin", ctypes.c_int), ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+                ("cout", ctypes.c_int), ("k_pad", ctypes.c_int),
+                ("kd", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),
+                ("sd", ctypes.c_int), ("sh", ctypes.c_int), ("sw", ctypes.c_int),
+                ("pd", ctypes.c_int), ("ph", ctypes.c_int), ("pw", ctypes.c_int),
+                ("od", ctypes.c_int), ("oh", ctypes.c_int), ("ow", ctypes.c_int),
+                ("out", ctypes.c_void_p), ("ldo", ctypes.c_int), ("c_off", ctypes.c_int),
+                ("residual", ctypes.c_void_p), ("ldr", ctypes.c_int), ("r_off", ctypes.c_int),
+                ("flags", ctypes.c_int)]
+
+
+class PoolDesc(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int), ("inp", ctypes.c_void_p),
+                ("n", ctypes.c_int), ("d", ctypes.c_int), ("h", ctypes.c_int), ("w", ctypes.c_int),
+                ("c", ctypes.c_int),
+                ("kd", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),
+                ("sd", ctypes.c_int), ("sh", ctypes.c_int), ("sw", ctypes.c_int),
+                ("pd", ctypes.c_int), ("ph", ctypes.c_int), ("pw", ctypes.c_int),
+                ("od", ctypes.c_int), ("oh", ctypes.c_int), ("ow", ctypes.c_int),
+                ("mode", ctypes.c_int), ("out", ctypes.c_void_p), ("ldo", ctypes.c_int), ("c_off", ctypes.c_int)]
+
+
+def _stream(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _triple(v):
+    if isinstance(v, int):
+        return (v, v, v)
+    v = tuple(v)
+    return (1,) * (3 - len(v)) + v if len(v) < 3 else v
+
+
+def _pads(v):
+    if isinstance(v, int):
+        return (v, v, v)
+    v = tuple(v)
+    return (0,) * (3 - len(v)) + v if len(v) < 3 else v
+
+
+def fold_bn(weight: torch.Tensor, bias, gamma, beta, mean, var, eps: float):
+    """Eval-mode BatchNorm folded into the preceding conv, in fp32 on the host:
+    s = gamma / sqrt(var + eps), W' = W s, b' = (b - mean) s + beta."""
+    w = weight.detach().to("cpu", torch.float32)
+    co = w.shape[0]
+    b = bias.detach().to("cpu", torch.float32) if bias is not None else torch.zeros(co)
+    if gamma is None:
+        return w, b
+    s = gamma.detach().float().cpu() / torch.sqrt(var.detach().float().cpu() + eps)
+    w = w * s.view(-1, *([1] * (w.dim() - 1)))
+    b = (b - mean.detach().float().cpu()) * s + beta.detach().float().cpu()
+    return w, b
+
+
+@dataclass
+class ConvGeom:
+    kd: int
+    kh: int
+    kw: int
+    sd: int
+    sh: int
+    sw: int
+    pd: int
+    ph: int
+    pw: int
+
+
+class ConvLayer:
+    """A conv (+ folded BN) packed for fac_conv_nd: weights 16-bit
+    [cout_pad][k_pad] with k = ((tz*kh + ty)*kw + tx)*cin_p + c."""
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor, stride=1, padding=0, *, dtype: str, device,
+                 cin_pad: int | None = None):
+        w = weight.detach().to("cpu", torch.float32)
+        if w.dim() == 4:                             # Conv2d: [co, ci, kh, kw] -> depth 1, no depth stride/pad
+            w = w.unsqueeze(2)
+            st = (1,) + ((stride, stride) if isinstance(stride, int) else tuple(stride))
+            pd = (0,) + ((padding, padding) if isinstance(padding, int) else tuple(padding))
+        else:
+            st, pd = _triple(stride), _pads(padding)
+        co, ci, kd, kh, kw = w.shape
+        self.cout, self.cin = co, ci
+        self.cin_p = cin_pad or (ci + 7) // 8 * 8
+        self.g = ConvGeom(kd, kh, kw, *st, *pd)
+        lib = _lib.load()
+        cp, kp = ctypes.c_int(), ctypes.c_int()
+        _lib.check(lib.fac_conv_weight_layout(co, self.cin_p, kd, kh, kw, ctypes.byref(cp), ctypes.byref(kp)), None,
+                   "fac_conv_weight_layout")
+        self.cout_pad, self.k_pad = cp.value, kp.value
+        wp = torch.zeros(co, kd, kh, kw, self.cin_p)
+        wp[..., :ci] = w.permute(0, 2, 3, 4, 1)
+        packed = torch.zeros(self.cout_pad, self.k_pad)
+        packed[:co, :kd * kh * kw * self.cin_p] = wp.reshape(co, -1)
+        self.dtype = dtype
+        self.w = packed.to(TORCH16[dtype]).to(device)
+        b = torch.zeros(self.cout_pad)
+        b[:co] = bias.detach().to("cpu", torch.float32)
+        self.b = b.to(device)
+
+    def out_dims(self, d, h, w):
+        g = self.g
+        return ((d + 2 * g.pd - g.kd) // g.sd + 1, (h + 2 * g.ph - g.kh) // g.sh + 1,
+                (w + 2 * g.pw - g.kw) // g.sw + 1)
+
+    def __call__(self, x: torch.Tensor, *, relu: bool = True, out: torch.Tensor | None = None, c_off: int = 0,
+                 residual: torch.Tensor | None = None, relu2: bool = False, out_f32: bool = False) -> torch.Tensor:
+        n, d, h, w, c = x.shape
+        if c != self.cin_p or x.dtype != TORCH16[self.dtype] or not x.is_contiguous():
+            raise ValueError(f"conv input must be contiguous {self.dtype} [N,D,H,W,{self.cin_p}], got "
+                             f"{x.dtype} {tuple(x.shape)}")
+        od, oh, ow = self.out_dims(d, h, w)
+        if out is None:
+            out = torch.empty(n, od, oh, ow, self.cout, device=x.device,
+                              dtype=torch.float32 if out_f32 else x.dtype)
+        if tuple(out.shape[:4]) != (n, od, oh, ow) or not out.is_contiguous():
+            raise ValueError(f"conv output must be contiguous [{n},{od},{oh},{ow},C], got {tuple(out.shape)}")
+        g = self.g
+        dsc = ConvDesc()
+        dsc.dtype = _lib.DTYPES[self.dtype]
+        dsc.inp = x.data_ptr()
+        dsc.n, dsc.d, dsc.h, dsc.w, dsc.cin = n, d, h, w, c
+        dsc.weight, dsc.bias = self.w.data_ptr(), self.b.data_ptr()
+        dsc.cout, dsc.k_pad = self.cout, self.k_pad
+        dsc.kd, dsc.kh, dsc.kw, dsc.sd, dsc.sh, dsc.sw = g.kd, g.kh, g.kw, g.sd, g.sh, g.sw
+        dsc.pd, dsc.ph, dsc.pw = g.pd, g.ph, g.pw
+        dsc.od, dsc.oh, dsc.ow = od, oh, ow
+        dsc.out, dsc.ldo, dsc.c_off = out.data_ptr(), out.shape[4], c_off
+        flags = (RELU if relu else 0) | (RELU2 if relu2 else 0) | (OUT_F32 if out_f32 else 0)
+        if residual is not None:
+            if tuple(residual.shape[:4]) != (n, od, oh, ow) or residual.dtype != x.dtype:
+                raise ValueError("residual must match the output positions and dtype")
+            dsc.residual, dsc.ldr, dsc.r_off = residual.data_ptr(), residual.shape[4], 0
+            flags |= RESID
+        dsc.flags = flags
+        _lib.check(_lib.load().fac_conv_nd(ctypes.byref(dsc), _stream(x)), None, "fac_conv_nd")
+        return out
+
+
+def pool(x: torch.Tensor, kernel, stride, padding=0, mode: str = "max", out: torch.Tensor | None = None,
+         c_off: int = 0) -> torch.Tensor:
+    n, d, h, w, c = x.shape
+    (kd, kh, kw), (sd, sh, sw), (pd, ph, pw) = _triple(kernel), _triple(stride), _pads(padding)
+    od, oh, ow = (d + 2 * pd - kd) // sd + 1, (h + 2 * ph - kh) // sh + 1, (w + 2 * pw - kw) // sw + 1
+    if out is None:
+        out = torch.empty(n, od, oh, ow, c, device=x.device, dtype=x.dtype)
+    dsc = PoolDesc()
+    dsc.dtype = 0 if x.dtype == torch.bfloat16 else 1
+    dsc.inp = x.data_ptr()
+    dsc.n, dsc.d, dsc.h, dsc.w, dsc.c = n, d, h, w, c
+    dsc.kd, dsc.kh, dsc.kw, dsc.sd, dsc.sh, dsc.sw, dsc.pd, dsc.ph, dsc.pw = kd, kh, kw, sd, sh, sw, pd, ph, pw
+    dsc.od, dsc.oh, dsc.ow = od, oh, ow
+    dsc.mode = {"max": 0, "avg": 1}[mode]
+    dsc.out, dsc.ldo, dsc.c_off = out.data_ptr(), out.shape[4], c_off
+    _lib.check(_lib.load().fac_pool_nd(ctypes.byref(dsc), _stream(x)), None, "fac_pool_nd")
+    return out
+
+
+def pack_input(src: torch.Tensor, *, dtype: str, u8: bool, div: float = 1.0, mean=None, std=None,
+               spatial: tuple[int, ...]) -> torch.Tensor:
+    """3-channel images -> 16-bit [N, D, H, W, 8] (fac_pack_input).
+    u8: src uint8 [N, *spatial, 3]; else fp32 planar [N, 3, *spatial]."""
+    n = src.shape[0]
+    s = 1
+    for v in spatial:
+        s *= v
+    d, h, w = (1,) * (3 - len(spatial)) + tuple(spatial)
+    out = torch.empty(n, d, h, w, 8, device=src.device, dtype=TORCH16[dtype])
+    m = (ctypes.c_float * 3)(*(mean if mean is not None else (0.0, 0.0, 0.0)))
+    sd = (ctypes.c_float * 3)(*(std if std is not None else (1.0, 1.0, 1.0)))
+    src = src.contiguous()
+    _lib.check(_lib.load().fac_pack_input(_lib.DTYPES[dtype], src.data_ptr(), 0 if u8 else 1, n, s, float(div),
+                                          ctypes.cast(m, ctypes.c_void_p), ctypes.cast(sd, ctypes.c_void_p),
+                                          out.data_ptr(), 8, _stream(src)), None, "fac_pack_input")
+    return out
+
+
+class KANLinearLayer:
+    """KANLinear (CViT-main/ResVitKan/kan.py:18-206) packed for fac_kan_linear:
+    wcat[o][i][0] = base_weight, wcat[o][i][1+k] = spline_weight * spline_scaler."""
+
+    N_KNOTS = 12
+
+    def __init__(self, grid, base_weight, spline_weight, spline_scaler, device):
+        g = grid.detach().to("cpu", torch.float32)
+        bw = base_weight.detach().to("cpu", torch.float32)
+        sw = spline_weight.detach().to("cpu", torch.float32)
+        ss = spline_scaler.detach().to("cpu", torch.float32)
+        self.out_f, self.in_f = bw.shape
+        if g.shape != (self.in_f, self.N_KNOTS) or sw.shape != (self.out_f, self.in_f, self.N_KNOTS - 4):
+            raise ValueError("KANLinear with grid_size 5 and spline_order 3 expected")
+        scaled = sw * ss.unsqueeze(-1)                    # scaled_spline_weight (kan.py:176-183)
+        self.wcat = torch.cat([bw.unsqueeze(-1), scaled], dim=2).contiguous().to(device)
+        self.grid = g.contiguous().to(device)
+        self._scratch = None
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        rows = x.shape[0]
+        lib = _lib.load()
+        nbytes = lib.fac_kan_scratch_bytes(rows, self.in_f, self.out_f)
+        if self._scratch is None or self._scratch.numel() * 4 < nbytes or self._scratch.device != x.device:
+            self._scratch = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=x.device)
+        y = torch.empty(rows, self.out_f, dtype=torch.float32, device=x.device)
+        x = x.contiguous()
+        _lib.check(lib.fac_kan_linear(x.data_ptr(), rows, self.in_f, self.out_f, self.grid.data_ptr(), self.N_KNOTS,
+                                      self.wcat.data_ptr(), y.data_ptr(), self._scratch.data_ptr(), _stream(x)),
+                   None, "fac_kan_linear")
+        return y
+
+
+def sigmoid(x: torch.Tensor) -> torch.Tensor:
+    y = torch.empty_like(x)
+    _lib.check(_lib.load().fac_sigmoid(x.data_ptr(), y.data_ptr(), x.numel(), _stream(x)), None, "fac_sigmoid")
+    return y

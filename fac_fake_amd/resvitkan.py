@@ -1,0 +1,240 @@
+"""Drop-in ``ResVitKan`` (BASELINE config 5) on gfx950 HIP kernels.
+
+Mirrors ``CViT-main/ResVitKan/ResVitKan.py::CViT`` (:284-329): the same
+constructor, the same 408-key ``state_dict`` (names, shapes, order — the
+``resnet50()`` stem, embedding, transformer, ``kan_head`` and the unused
+``mlp_head``) and ``forward(img, mask=None)`` on a normalised fp32 NCHW
+``[B,3,224,224]`` batch returning fp32 logits ``[B,2]`` (eval mode: Dropout is
+the identity), with the reference's batch-slot ``pos_embedding`` rule.
+
+Arithmetic (no CPU fallback, every layer is a HIP kernel of libfac_cvit.so):
+
+* ResNet-50 stem: each conv + eval BatchNorm (folded on the host in fp32,
+  weights rounded once to 16 bits) is one ``fac_conv_nd`` implicit-GEMM launch
+  (fac_fake_amd/csrc/ops.hip); the Bottleneck's conv3 epilogue applies bn3,
+  ReLU, the residual add and the second ReLU in fp32 (ResVitKan.py:146-152);
+  the 3x3/2 max-pool is ``fac_pool_nd``.  Activations are 16-bit NHWC.
+* ``channel`` 1x1 + bn2 -> features [B,7,7,512] NHWC, which is already the
+  ``(p1 p2 c)`` flatten of ResVitKan.py:320, handed to the CViT tail
+  (``fac_forward_features``: patch embedding, cls/pos, 6-layer transformer,
+  ``kan_head.0`` + ReLU) — the CViT kernels, loaded "tail_only".
+* ``KAN([2048, 64, 2])``: two ``fac_kan_linear`` launches in fp32.
+
+The whole forward can be captured into a hipGraph (``torch.cuda.graph``):
+every launch goes to the current torch stream, workspaces come from torch's
+caching allocator.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+from torch import nn
+
+from . import _lib
+from .cvit import MAX_SLOTS, _Node
+from .ops import TORCH16, ConvLayer, KANLinearLayer, fold_bn, pack_input, pool, sigmoid
+from .weights import kan_grid, resnet50_blocks, resvitkan_param_specs
+
+SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
+                 mlp_dim=2048)
+BN_EPS = 1e-5
+MEAN = (0.485, 0.456, 0.406)     # helpers/loader.py:9 (the training normalisation)
+STD = (0.229, 0.224, 0.225)
+_BUFFERS = ("rmean", "rvar", "nbt", "kgrid")
+
+
+def _init_tensor(name, shape, kind):
+    if kind == "nbt":
+        return torch.zeros((), dtype=torch.long)
+    if kind in ("rmean", "beta", "lbias"):
+        return torch.zeros(shape)
+    if kind in ("rvar", "gamma", "gamma_res"):
+        return torch.ones(shape)
+    if kind == "emb":
+        return torch.randn(shape)
+    if kind == "kgrid":
+        return torch.from_numpy(kan_grid(shape[0]))
+    t = torch.empty(shape)
+    fan_in = int(math.prod(shape[1:]))
+    if kind == "conv":
+        return t.normal_(0, math.sqrt(2.0 / fan_in))
+    bound = 1.0 / math.sqrt(shape[1] if len(shape) > 1 else 1)
+    return t.uniform_(-bound, bound)
+
+
+class ResVitKan(nn.Module):
+    def __init__(self, image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
+                 mlp_dim=2048, *, dtype: str = "bf16"):
+        super().__init__()
+        cfg = dict(image_size=image_size, patch_size=patch_size, num_classes=num_classes, channels=channels, dim=dim,
+                   depth=depth, heads=heads, mlp_dim=mlp_dim)
+        if cfg != SUPPORTED:
+            raise NotImplementedError(f"the gfx950 ResVitKan path implements {SUPPORTED}, got {cfg}")
+        if dtype not in _lib.DTYPES:
+            raise ValueError(f"dtype must be one of {list(_lib.DTYPES)}")
+        self.dtype_name = dtype
+        self.patch_size = patch_size
+        for name, shape, kind in resvitkan_param_specs(dim=dim, depth=depth, mlp_dim=mlp_dim,
+                                                       num_classes=num_classes, channels=channels,
+                                                       patch_size=patch_size):
+            *path, leaf = name.split(".")
+            mod = self
+            for p in path:
+                if p not in mod._modules:
+                    mod.add_module(p, _Node())
+                mod = mod._modules[p]
+            t = _init_tensor(name, shape, kind)
+            if kind in _BUFFERS:
+                mod.register_buffer(leaf, t)
+            else:
+                mod.register_parameter(leaf, nn.Parameter(t))
+        self._prep = None          # (device index, versions) the packed layers belong to
+        self._ctx = None
+        self.eval()
+
+    # ------------------------------------------------------------------ weights
+    def _versions(self):
+        return tuple(t._version for t in self.state_dict(keep_vars=True).values()) + (
+            tuple(t.data_ptr() for t in self.parameters()),)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._prep = None
+        return out
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise RuntimeError("the gfx950 ResVitKan path is inference-only (BatchNorm is folded into the convs)")
+        return super().train(False)
+
+    def _release(self):
+        if self._ctx is not None:
+            _lib.load().fac_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    def _prepare(self, device: torch.device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        v = self._versions()
+        if self._prep == (idx, v):
+            return
+        sd = self.state_dict()
+        dt = self.dtype_name
+
+        def conv(ck, bnp, stride=1, pad=0, cin_pad=None):
+            w, b = fold_bn(sd[ck], None, sd[bnp + ".weight"], sd[bnp + ".bias"], sd[bnp + ".running_mean"],
+                           sd[bnp + ".running_var"], BN_EPS)
+            return ConvLayer(w, b, stride, pad, dtype=dt, device=device, cin_pad=cin_pad)
+
+        self._conv1 = conv("features.conv1.weight", "features.bn1", 2, 3, cin_pad=8)
+        self._blocks = []
+        for p, _inp, _planes, s, ds in resnet50_blocks():
+            self._blocks.append((conv(p + ".conv1.weight", p + ".bn1"),
+                                 conv(p + ".conv2.weight", p + ".bn2", s, 1),
+                                 conv(p + ".conv3.weight", p + ".bn3"),
+                                 conv(p + ".downsample.0.weight", p + ".downsample.1", s) if ds else None))
+        self._channel = conv("features.channel.weight", "features.bn2")
+        self._kan = [KANLinearLayer(sd[f"kan_head.3.layers.{i}.grid"], sd[f"kan_head.3.layers.{i}.base_weight"],
+                                    sd[f"kan_head.3.layers.{i}.spline_weight"],
+                                    sd[f"kan_head.3.layers.{i}.spline_scaler"], device) for i in range(2)]
+        # the CViT tail (embedding .. first head layer), loaded without a conv stem
+        lib = _lib.load()
+        self._release()
+        h = ctypes.c_void_p()
+        _lib.check(lib.fac_create(idx, _lib.DTYPES[dt], ctypes.byref(h)), None, "fac_create")
+        self._ctx = h
+        _lib.check(lib.fac_set_option(h, b"tail_only", 1), h, "fac_set_option")
+        tail = {k: t for k, t in sd.items() if k in ("pos_embedding", "cls_token") or
+                k.startswith("patch_to_embedding.") or k.startswith("transformer.")}
+        tail["mlp_head.0.weight"] = sd["kan_head.0.weight"]
+        tail["mlp_head.0.bias"] = sd["kan_head.0.bias"]
+        tail["mlp_head.2.weight"] = torch.zeros(2, sd["kan_head.0.weight"].shape[0])  # unused: logits come from the KAN
+        tail["mlp_head.2.bias"] = torch.zeros(2)
+        keep, descs = [], []
+        for k, t in tail.items():
+            hst = t.detach().to("cpu", torch.float32).contiguous()
+            keep.append(hst)
+            d = _lib.TensorDesc()
+            d.name, d.data, d.ndim = k.encode(), hst.data_ptr(), hst.dim()
+            for i, s in enumerate(hst.shape):
+                d.shape[i] = s
+            descs.append(d)
+        arr = (_lib.TensorDesc * len(descs))(*descs)
+        _lib.check(lib.fac_load_weights(h, ctypes.cast(arr, ctypes.c_void_p), len(descs)), h, "fac_load_weights")
+        self._prep = (idx, v)
+
+    def reserve(self, max_batch: int, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._prepare(dev)
+        _lib.check(_lib.load().fac_reserve(self._ctx, int(max_batch)), self._ctx, "fac_reserve")
+
+    # ------------------------------------------------------------------ forward
+    def features16(self, x16: torch.Tensor) -> torch.Tensor:
+        """ResNet.forward (ResVitKan.py:232-247) on packed 16-bit [B,1,224,224,8]
+        -> [B,1,7,7,512] 16-bit NHWC."""
+        x = self._conv1(x16)                                        # 7x7/2 + bn1 + ReLU
+        x = pool(x, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")         # MaxPool2d(3, 2, 1)
+        for c1, c2, c3, ds in self._blocks:
+            res = ds(x, relu=False) if ds is not None else x
+            h = c2(c1(x))
+            x = c3(h, residual=res, relu2=True)                     # relu(bn3) + residual, relu
+        return self._channel(x, relu=False)                         # channel 1x1 + bn2
+
+    def _run(self, x16: torch.Tensor, pos_index, want_probs: bool):
+        B = x16.shape[0]
+        dev = x16.device
+        pidx = _pos_index(B, pos_index, dev)
+        f = self.features16(x16)
+        hidden = torch.empty(B, SUPPORTED["mlp_dim"], dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        _lib.check(lib.fac_forward_features(self._ctx, f.data_ptr(), B, pidx.data_ptr(), hidden.data_ptr(), None,
+                                            None, torch.cuda.current_stream(dev).cuda_stream), self._ctx,
+                   "fac_forward_features")
+        logits = self._kan[1](self._kan[0](hidden))
+        return logits, (sigmoid(logits) if want_probs else None)
+
+    def forward(self, img: torch.Tensor, mask=None, pos_index=None) -> torch.Tensor:
+        if mask is not None:
+            raise NotImplementedError("mask is not supported by the HIP path")
+        if not img.is_cuda:
+            raise RuntimeError("ResVitKan (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
+        if img.dim() != 4 or tuple(img.shape[1:]) != (3, 224, 224):
+            raise ValueError(f"expected img [B,3,224,224], got {tuple(img.shape)}")
+        self._prepare(img.device)
+        x16 = pack_input(img.float(), dtype=self.dtype_name, u8=False, spatial=(224, 224))
+        return self._run(x16, pos_index, False)[0]
+
+    def forward_u8(self, crops: torch.Tensor, pos_index=None, return_probs: bool = False):
+        """uint8 NHWC RGB crops [B,224,224,3]; x/255 + ImageNet Normalize fused into the input packing."""
+        if crops.dtype != torch.uint8 or crops.dim() != 4 or tuple(crops.shape[1:]) != (224, 224, 3):
+            raise ValueError(f"expected uint8 crops [B,224,224,3], got {crops.dtype} {tuple(crops.shape)}")
+        if not crops.is_cuda:
+            raise RuntimeError("ResVitKan (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
+        self._prepare(crops.device)
+        x16 = pack_input(crops, dtype=self.dtype_name, u8=True, div=255.0, mean=MEAN, std=STD, spatial=(224, 224))
+        logits, probs = self._run(x16, pos_index, return_probs)
+        return (logits, probs) if return_probs else logits
+
+
+def _pos_index(B: int, pos_index, device) -> torch.Tensor:
+    if pos_index is None:
+        if B > MAX_SLOTS:   # `x += self.pos_embedding[0:shape]` (ResVitKan.py:324-325) raises past 32
+            raise RuntimeError(f"The size of tensor a ({B}) must match the size of tensor b ({MAX_SLOTS}) "
+                               f"at non-singleton dimension 0")
+        return torch.arange(B, dtype=torch.int32, device=device)
+    p = torch.as_tensor(pos_index)
+    if p.shape != (B,):
+        raise ValueError(f"pos_index must have shape ({B},), got {tuple(p.shape)}")
+    if p.numel() and (int(p.min()) < 0 or int(p.max()) >= MAX_SLOTS):
+        raise IndexError(f"pos_index values must lie in [0, {MAX_SLOTS})")
+    return p.to(device=device, dtype=torch.int32).contiguous()
+
+
+__all__ = ["ResVitKan", "TORCH16"]

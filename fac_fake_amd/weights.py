@@ -160,3 +160,110 @@ def state_dict_checksums(sd) -> dict:
     """Per-tensor float64 sum / abs-sum, for pinning the generator in tests."""
     return {k: (float(np.asarray(v, np.float64).sum()), float(np.abs(np.asarray(v, np.float64)).sum()))
             for k, v in sd.items()}
+
+
+# ---------------------------------------------------------------- ResVitKan
+# CViT-main/ResVitKan/ResVitKan.py: resnet50() stem (Bottleneck [3,4,6,3],
+# :259-264) + `channel` 1x1 2048->512 + bn2 (:202-203), the CViT embedding /
+# transformer (:284-302), kan_head = Linear -> Dropout -> ReLU -> KAN([2048,
+# 64, 2]) (:302-307) and the unused mlp_head (:309-314).
+RESNET50_LAYERS = [(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]  # (planes, blocks, stride)
+KAN_GRID_SIZE, KAN_ORDER = 5, 3
+
+
+def resnet50_blocks():
+    """(prefix, inplanes, planes, stride, has_downsample) per Bottleneck, in
+    _make_layer order (ResVitKan.py:216-230)."""
+    out, inplanes = [], 64
+    for li, (planes, blocks, stride) in enumerate(RESNET50_LAYERS):
+        for b in range(blocks):
+            s = stride if b == 0 else 1
+            ds = b == 0 and (s != 1 or inplanes != planes * 4)
+            out.append((f"features.layer{li + 1}.{b}", inplanes, planes, s, ds))
+            inplanes = planes * 4
+    return out
+
+
+def _bn_specs(p, c, gamma_kind="gamma"):
+    return [(f"{p}.weight", (c,), gamma_kind), (f"{p}.bias", (c,), "beta"), (f"{p}.running_mean", (c,), "rmean"),
+            (f"{p}.running_var", (c,), "rvar"), (f"{p}.num_batches_tracked", (), "nbt")]
+
+
+def resvitkan_param_specs(dim=1024, depth=6, mlp_dim=2048, num_classes=2, channels=512, patch_size=7):
+    """(name, shape, kind) for every key of ResVitKan.CViT's state_dict, in its order (408 keys)."""
+    specs = [("pos_embedding", (32, 1, dim), "emb"), ("cls_token", (1, 1, dim), "emb"),
+             ("features.conv1.weight", (64, 3, 7, 7), "conv")]
+    specs += _bn_specs("features.bn1", 64)
+    for p, inp, planes, _s, ds in resnet50_blocks():
+        specs += [(f"{p}.conv1.weight", (planes, inp, 1, 1), "conv")] + _bn_specs(f"{p}.bn1", planes)
+        specs += [(f"{p}.conv2.weight", (planes, planes, 3, 3), "conv")] + _bn_specs(f"{p}.bn2", planes)
+        specs += [(f"{p}.conv3.weight", (planes * 4, planes, 1, 1), "conv")] + _bn_specs(f"{p}.bn3", planes * 4,
+                                                                                          "gamma_res")
+        if ds:
+            specs += [(f"{p}.downsample.0.weight", (planes * 4, inp, 1, 1), "conv")]
+            specs += _bn_specs(f"{p}.downsample.1", planes * 4)
+    specs += [("features.channel.weight", (channels, 2048, 1, 1), "conv")] + _bn_specs("features.bn2", channels)
+    pdim = channels * patch_size ** 2
+    specs += [("patch_to_embedding.weight", (dim, pdim), "lin"), ("patch_to_embedding.bias", (dim,), "lbias")]
+    specs += [s for s in cvit_param_specs(dim, depth, mlp_dim, num_classes, channels, patch_size)
+              if s[0].startswith("transformer.")]
+    specs += [("kan_head.0.weight", (mlp_dim, dim), "lin"), ("kan_head.0.bias", (mlp_dim,), "lbias")]
+    nb = KAN_GRID_SIZE + KAN_ORDER
+    for i, (fi, fo) in enumerate([(mlp_dim, 64), (64, num_classes)]):
+        p = f"kan_head.3.layers.{i}"
+        specs += [(f"{p}.base_weight", (fo, fi), "kbase"), (f"{p}.spline_weight", (fo, fi, nb), "kspline"),
+                  (f"{p}.spline_scaler", (fo, fi), "kscaler"),
+                  (f"{p}.grid", (fi, KAN_GRID_SIZE + 2 * KAN_ORDER + 1), "kgrid")]
+    specs += [("mlp_head.0.weight", (mlp_dim, dim), "lin"), ("mlp_head.0.bias", (mlp_dim,), "lbias"),
+              ("mlp_head.3.weight", (num_classes, mlp_dim), "head"), ("mlp_head.3.bias", (num_classes,), "lbias")]
+    return specs
+
+
+def kan_grid(in_features: int) -> np.ndarray:
+    """KANLinear's initial knot buffer (kan.py:39-48): arange(-3, 9) * 0.4 - 1 in float32."""
+    h = np.float32((1 - (-1)) / KAN_GRID_SIZE)
+    k = np.arange(-KAN_ORDER, KAN_GRID_SIZE + KAN_ORDER + 1).astype(np.float32)
+    g = (k * h).astype(np.float32) + np.float32(-1)
+    return np.broadcast_to(g.astype(np.float32), (in_features, g.size)).copy()
+
+
+def make_resvitkan_state_dict(seed: int = 0, **kw) -> "OrderedDict[str, np.ndarray]":
+    """Synthetic ResVitKan weights (same scheme as make_state_dict).  The last
+    BN of every Bottleneck gets a small gamma (0.1..0.3) so the residual
+    stream of 16 blocks stays O(1) (the non-standard ReLU-before-add of
+    ResVitKan.py:146-152 only ever adds), and the KAN weights are scaled for
+    O(1), unsaturated logits."""
+    sd = OrderedDict()
+    for name, shape, kind in resvitkan_param_specs(**kw):
+        if kind == "nbt":
+            sd[name] = np.array(0, dtype=np.int64)
+        elif kind == "conv":
+            fan_in = int(np.prod(shape[1:]))
+            a = float(np.sqrt(6.0 / fan_in))
+            sd[name] = _u(name, shape, seed, -a, a)
+        elif kind == "gamma_res":
+            sd[name] = _u(name, shape, seed, 0.1, 0.3)
+        elif kind == "kgrid":
+            sd[name] = kan_grid(shape[0])
+        elif kind in ("kbase", "kscaler"):
+            # the 64 -> 2 layer is scaled up so the logits are O(1)
+            a = float((8.0 if ".layers.1." in name else 1.0) / np.sqrt(shape[1]))
+            sd[name] = _u(name, shape, seed, -a, a)
+        elif kind == "kspline":
+            sd[name] = _u(name, shape, seed, -0.5, 0.5)
+        else:
+            sd[name] = _synthetic(name, shape, kind, seed)
+    return sd
+
+
+def _synthetic(name, shape, kind, seed):
+    if kind == "lin":
+        a = float(1.0 / np.sqrt(shape[1]))
+        return _u(name, shape, seed, -a, a)
+    if kind == "head":
+        a = float(4.0 / np.sqrt(shape[1]))
+        return _u(name, shape, seed, -a, a)
+    ranges = {"emb": (-0.5, 0.5), "cbias": (-0.05, 0.05), "lbias": (-0.02, 0.02), "gamma": (0.8, 1.2),
+              "beta": (-0.1, 0.1), "rmean": (-0.1, 0.1), "rvar": (0.8, 1.2)}
+    lo, hi = ranges[kind]
+    return _u(name, shape, seed, lo, hi)

@@ -83,6 +83,18 @@ int fac_forward_nchw_f32(fac_ctx* ctx, const float* d_in, int B, const int32_t* 
 int fac_forward_nhwc_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
                         float* d_probs, void* stream);
 
+/* Everything after the conv stem (cvit.py:170-179): d_feat = 16-bit NHWC
+ * stem features [B,7,7,512] (the (p1 p2 c) flatten of cvit.py:170) ->
+ * patch embedding, cls/pos, transformer, head.  d_hidden (fp32 [B,2048],
+ * or NULL) receives ReLU(mlp_head.0(cls)); d_logits/d_probs (or NULL) the
+ * final layer.  With fac_set_option(ctx, "tail_only", 1) before
+ * fac_load_weights only the embedding/transformer/head keys are needed:
+ * ResVitKan (CViT-main/ResVitKan/ResVitKan.py:316-329) shares this tail
+ * behind its ResNet-50 stem, with kan_head.0 as mlp_head.0 and the KAN
+ * (fac_ops.h) on d_hidden. */
+int fac_forward_features(fac_ctx* ctx, const void* d_feat, int B, const int32_t* d_pos_index, float* d_hidden,
+                         float* d_logits, float* d_probs, void* stream);
+
 /* Software-pipelined forward for streams of batches (a video-scoring
  * server; bench.py's default mode).  Enqueues batch k's conv stack on
  * `stream` (into one of two context-owned stem buffers) and its patch
@@ -151,7 +163,8 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * pool as one fused kernel, the default; 0 = one kernel per conv),
  * "gemm_patch" / "gemm_qkv" / "gemm_out" / "gemm_ff1" / "gemm_ff2" /
  * "gemm_head" (GEMM tile variant -1..3 per call site), "proj_splits" (split-K
- * of to_out and FF2: 1, 2 or 4). */
+ * of to_out and FF2: 1, 2 or 4), "tail_only" (before fac_load_weights: no
+ * conv stem, fac_forward_features only), "tail_priority". */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);

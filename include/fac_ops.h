@@ -1,0 +1,120 @@
+/* fac_ops.h — C ABI of the layer-level gfx950 kernels behind the §8f model
+ * families: ResVitKan (config 5) and S3D (config 4).
+ *
+ * The CViT path has one fused entry point per forward (fac_cvit.h); the
+ * ResNet-50 stem of ResVitKan and the Inception-3D blocks of S3D are
+ * sequences of ordinary layers, orchestrated by their Python mirrors
+ * (fac_fake_amd/resvitkan.py, fac_fake_amd/s3d.py) and captured into one
+ * hipGraph per forward.  Every entry point is stream-ordered, takes device
+ * pointers and plain sizes, returns 0 or a negative fac_status
+ * (fac_cvit.h) and never throws.
+ *
+ * Activations are 16-bit (bf16 or fp16, `dtype` as in fac_cvit.h)
+ * channels-last N·D·H·W·C tensors, C a multiple of 8 (inputs with 3
+ * channels are packed to 8 by fac_pack_input).  2-D layers are D = 1.
+ */
+#ifndef FAC_OPS_H
+#define FAC_OPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Epilogue flags of fac_conv_nd. */
+#define FAC_CONV_RELU 1      /* v = max(acc + bias, 0) */
+#define FAC_CONV_RESID 2     /* v = v + residual[m][r_off + c] (16-bit) */
+#define FAC_CONV_RELU2 4     /* v = max(v, 0) after the residual */
+#define FAC_CONV_OUT_F32 8   /* fp32 output instead of 16-bit */
+
+/* One N-d convolution (Conv2d / Conv3d, any kernel, stride, zero padding,
+ * dilation 1, groups 1) with folded BatchNorm, as an implicit GEMM on MFMA:
+ * rows = output positions (n, z, y, x), columns = output channels,
+ * k = (tap, input channel).
+ *
+ * Replaces nn.Conv2d + nn.BatchNorm2d(eval) (+ nn.ReLU, + the residual add
+ * of a ResNet Bottleneck) — CViT-main/ResVitKan/ResVitKan.py:124-152,
+ * :187-200, :232-240 — and nn.Conv3d + BatchNorm3d(eval) + ReLU of S3D's
+ * BasicConv3d / SepConv3d — sx_exp_deepfakedetect-master/S3D/model.py:50-82.
+ *
+ * weight: 16-bit [cout_pad][k_pad], row o = output channel, k index =
+ *   ((tz*kh + ty)*kw + tx)*cin + c, zero beyond taps*cin; cout_pad a
+ *   multiple of 128, k_pad a multiple of 32 (fac_conv_weight_layout).
+ * bias: fp32 [cout_pad] (BN shift folded in).
+ * out: row m = ((n*Do + z)*Ho + y)*Wo + x, element [m*ldo + c_off + c];
+ *   c_off lets Inception branches write straight into their concat slot.
+ * residual (FAC_CONV_RESID): 16-bit [m*ldr + r_off + c]. */
+typedef struct fac_conv_desc {
+  int dtype;
+  const void* in;
+  int n, d, h, w, cin;          /* input dims; cin % 8 == 0 */
+  const void* weight;
+  const float* bias;
+  int cout, k_pad;              /* k_pad: weight row length (elements) */
+  int kd, kh, kw;               /* kernel */
+  int sd, sh, sw;               /* stride */
+  int pd, ph, pw;               /* zero padding */
+  int od, oh, ow;               /* output dims (floor mode) */
+  void* out;
+  int ldo, c_off;
+  const void* residual;
+  int ldr, r_off;
+  int flags;
+} fac_conv_desc;
+
+int fac_conv_nd(const fac_conv_desc* desc, void* stream);
+
+/* Weight packing geometry for fac_conv_nd: *cout_pad = cout rounded up to
+ * 128, *k_pad = taps*cin rounded up to 32. */
+int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad);
+
+/* Max or average pooling, channels-last 16-bit (MaxPool2d/3d: padding is
+ * -inf, i.e. ignored; AvgPool: count_include_pad=True, the PyTorch default).
+ * mode 0 = max, 1 = avg.  out element [m*ldo + c_off + c].
+ * Replaces nn.MaxPool2d(3, 2, 1) (ResVitKan.py:205), S3D's nn.MaxPool3d
+ * layers and F.avg_pool3d (S3D/model.py:31-45). */
+typedef struct fac_pool_desc {
+  int dtype;
+  const void* in;
+  int n, d, h, w, c;
+  int kd, kh, kw, sd, sh, sw, pd, ph, pw;
+  int od, oh, ow;
+  int mode;
+  void* out;
+  int ldo, c_off;
+} fac_pool_desc;
+
+int fac_pool_nd(const fac_pool_desc* desc, void* stream);
+
+/* Input staging: 3-channel images -> 16-bit channels-last with c_pad
+ * channels (zeros beyond 3): out[n][s][c] = (x / div - mean[c]) / std[c]
+ * in fp32.  src_kind 0: uint8 [n][s][3] (face crops: div = 255 gives the
+ * reference's x/255. then Normalize, cvit_prediction.py:214-215);
+ * src_kind 1: fp32 planar [n][3][s] (an already normalised NCHW tensor, or
+ * S3D's raw 0..255 NCTHW clip: div 1, mean 0, std 1).  s = spatial
+ * positions per image; mean3/std3 may be NULL (0 / 1). */
+int fac_pack_input(int dtype, const void* src, int src_kind, int n, int s, float div, const float* mean3,
+                   const float* std3, void* out, int c_pad, void* stream);
+
+/* KANLinear forward (CViT-main/ResVitKan/kan.py:189-206), fp32:
+ *   y = silu(x) · base_weightᵀ + b_splines(x) · (spline_weight ⊙ spline_scaler)ᵀ
+ * with order-3 B-spline bases over the per-feature knot vector `grid`
+ * [in][n_knots] (kan.py:90-132, the Cox–de Boor recursion in the
+ * reference's operation order).  `wcat` is the fused weight [out][in][1 + nb]
+ * (column 0 = base_weight, 1.. = scaled spline weights, nb = n_knots - 4).
+ * x [rows][in] fp32 -> y [rows][out] fp32.  `partial` is a scratch buffer of
+ * fac_kan_scratch_bytes() bytes. */
+int fac_kan_linear(const float* x, int rows, int in_f, int out_f, const float* grid, int n_knots, const float* wcat,
+                   float* y, void* partial, void* stream);
+size_t fac_kan_scratch_bytes(int rows, int in_f, int out_f);
+
+/* Row-wise sigmoid of logits (the per-logit pred_sig of the heads). */
+int fac_sigmoid(const float* x, float* y, int n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FAC_OPS_H */

@@ -1,0 +1,193 @@
+"""Layer kernels of include/fac_ops.h and the ResVitKan drop-in on the GPU.
+
+* fac_conv_nd vs a plain PyTorch fp32 convolution (CPU) of the same 16-bit
+  operands: bit-equal after rounding except for accumulation-order flips of
+  one 16-bit ulp (<= 1 ulp everywhere, on <= 5% of the outputs) — over 2-D and
+  3-D kernels, strides, paddings, ragged channel counts, fp32 output, concat
+  offsets and the Bottleneck residual epilogue.
+* fac_pool_nd: bit-exact (max) / within fp32 rounding of one 16-bit ulp (avg).
+* fac_kan_linear vs the reference's KANLinear outputs (golden): <= 1e-5.
+* ResVitKan forward vs the reference module's logits (golden, fp32):
+  per-logit sigmoid within 1e-3 with fp16 operands and 1e-2 with bf16
+  (the emulated rounding alone moves bf16 by ~2e-3, tests/test_resvitkan.py).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fac_fake_amd.weights import make_crops, make_resvitkan_state_dict
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+T16 = {"bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def _ulps(a: torch.Tensor, b: torch.Tensor, dt: str) -> torch.Tensor:
+    """|a - b| in units of the 16-bit ulp at max(|a|, |b|), after allowing the
+    fp32 accumulation noise of a K-term dot product (2^-16 of the output
+    scale: outputs that are the small difference of O(1) partial sums carry
+    fp32 rounding a few fp16 ulps of their own size)."""
+    a, b = a.float(), b.float()
+    m = torch.maximum(a.abs(), b.abs()).clamp_min(1e-30)
+    e = torch.floor(torch.log2(m))
+    ulp = torch.pow(2.0, e - (7 if dt == "bf16" else 10))
+    if dt == "fp16":
+        ulp = ulp.clamp_min(2.0 ** -24)   # fp16 subnormals: fixed spacing
+    noise = 2.0 ** -16 * torch.maximum(a.abs().max(), b.abs().max())
+    return ((a - b).abs() - noise).clamp_min(0) / ulp
+
+
+CONV_CASES = [
+    # (n, d, h, w, cin, cout, k(kd,kh,kw), stride, pad)
+    (2, 1, 17, 19, 64, 64, (1, 1, 1), 1, 0),
+    (2, 1, 14, 14, 64, 200, (1, 3, 3), 1, (0, 1, 1)),
+    (2, 1, 15, 15, 128, 96, (1, 3, 3), (1, 2, 2), (0, 1, 1)),
+    (1, 1, 40, 40, 8, 64, (1, 7, 7), (1, 2, 2), (0, 3, 3)),
+    (2, 1, 9, 9, 256, 512, (1, 1, 1), (1, 2, 2), 0),
+    (1, 6, 10, 10, 16, 32, (3, 1, 1), 1, (1, 0, 0)),
+    (1, 5, 12, 12, 24, 48, (1, 3, 3), 1, (0, 1, 1)),
+    (1, 8, 16, 16, 8, 64, (3, 7, 7), 2, (1, 3, 3)),
+    (1, 3, 7, 7, 40, 12, (1, 1, 1), 1, 0),
+]
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", range(len(CONV_CASES)))
+def test_conv_nd_vs_torch_fp32(case, dt):
+    from fac_fake_amd.ops import ConvLayer
+    n, d, h, w, cin, cout, k, st, pd = CONV_CASES[case]
+    g = torch.Generator().manual_seed(100 + case)
+    x = torch.randn(n, cin, d, h, w, generator=g).to(T16[dt]).float()
+    wt = (torch.randn(cout, cin, *k, generator=g) / np.sqrt(cin * np.prod(k))).float()
+    b = torch.randn(cout, generator=g) * 0.1
+    layer = ConvLayer(wt, b, st, pd, dtype=dt, device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    y = layer(xg, relu=True)
+    torch.cuda.synchronize()
+    ref = F.relu(F.conv3d(x, wt.to(T16[dt]).float(), b, stride=st, padding=pd)).permute(0, 2, 3, 4, 1)
+    yr = ref.to(T16[dt])
+    u = _ulps(y.cpu(), yr, dt)
+    assert tuple(y.shape) == tuple(yr.shape)
+    assert u.max() <= 1.0, (case, float(u.max()))
+    assert (u > 0).float().mean() <= 0.05
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+def test_conv_nd_residual_concat_and_f32(dt):
+    """Bottleneck epilogue relu(relu(conv + b) + res) into a channel slot of a
+    wider buffer; and fp32 output of a 1-channel conv (S3D's final layer)."""
+    from fac_fake_amd.ops import ConvLayer
+    g = torch.Generator().manual_seed(7)
+    n, h, w, cin, cout = 2, 11, 13, 32, 48
+    x = torch.randn(n, cin, 1, h, w, generator=g).to(T16[dt]).float()
+    wt = torch.randn(cout, cin, 1, 3, 3, generator=g) / 17.0
+    b = torch.randn(cout, generator=g) * 0.1
+    res = torch.randn(n, 1, h, w, cout, generator=g).to(T16[dt])
+    layer = ConvLayer(wt, b, 1, (0, 1, 1), dtype=dt, device=DEV)
+    big = torch.zeros(n, 1, h, w, 128, dtype=T16[dt], device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    layer(xg, relu=True, out=big[..., :], c_off=40, residual=None)
+    out2 = layer(xg, relu=True, residual=res.to(DEV), relu2=True)
+    torch.cuda.synchronize()
+    conv = F.conv3d(x, wt.to(T16[dt]).float(), b, padding=(0, 1, 1)).permute(0, 2, 3, 4, 1)
+    ref1 = F.relu(conv).to(T16[dt])
+    ref2 = F.relu(F.relu(conv) + res.float()).to(T16[dt])
+    bc = big.cpu()
+    assert _ulps(bc[..., 40:40 + cout], ref1, dt).max() <= 1.0
+    assert bc[..., :40].abs().max() == 0 and bc[..., 40 + cout:].abs().max() == 0
+    assert _ulps(out2.cpu(), ref2, dt).max() <= 1.0
+    one = ConvLayer(wt[:1], b[:1], 1, (0, 1, 1), dtype=dt, device=DEV)
+    y = one(xg, relu=False, out_f32=True)
+    torch.cuda.synchronize()
+    ref = F.conv3d(x, wt[:1].to(T16[dt]).float(), b[:1], padding=(0, 1, 1)).permute(0, 2, 3, 4, 1)
+    assert y.dtype == torch.float32 and torch.allclose(y.cpu(), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+def test_pool_nd(dt):
+    from fac_fake_amd.ops import pool
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 24, 5, 17, 17, generator=g).to(T16[dt])
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV)
+    ym = pool(xg, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")
+    y3 = pool(xg, (3, 3, 3), (2, 2, 2), (1, 1, 1), "max")
+    ya = pool(xg, (2, 17, 17), (2, 17, 17), 0, "avg")
+    torch.cuda.synchronize()
+    rm = F.max_pool3d(x.float(), (1, 3, 3), (1, 2, 2), (0, 1, 1)).permute(0, 2, 3, 4, 1)
+    r3 = F.max_pool3d(x.float(), 3, 2, 1).permute(0, 2, 3, 4, 1)
+    ra = F.avg_pool3d(x.float(), (2, 17, 17)).permute(0, 2, 3, 4, 1)
+    assert torch.equal(ym.cpu().float(), rm) and torch.equal(y3.cpu().float(), r3)
+    assert _ulps(ya.cpu(), ra.to(T16[dt]), dt).max() <= 1.0
+
+
+def test_kan_linear_vs_reference(golden):
+    from fac_fake_amd.ops import KANLinearLayer
+    g = golden("resvitkan_golden.npz")
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in make_resvitkan_state_dict(0).items()}
+    p = "kan_head.3.layers.0"
+    layer = KANLinearLayer(sd[p + ".grid"], sd[p + ".base_weight"], sd[p + ".spline_weight"],
+                           sd[p + ".spline_scaler"], DEV)
+    y = layer(torch.from_numpy(g["kan_x"]).to(DEV))
+    torch.cuda.synchronize()
+    assert np.abs(y.cpu().numpy() - g["kan_y"]).max() <= 1e-5
+
+
+@pytest.fixture(scope="module")
+def rvk():
+    from fac_fake_amd.resvitkan import ResVitKan
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in make_resvitkan_state_dict(0).items()}
+    out = {}
+    for dt in ("fp16", "bf16"):
+        m = ResVitKan(dtype=dt)
+        m.load_state_dict(sd)
+        out[dt] = m
+    return out
+
+
+@pytest.mark.parametrize("dt,tol", [("fp16", 1e-3), ("bf16", 1e-2)])
+def test_resvitkan_matches_reference(rvk, golden, dt, tol):
+    from oracle.cvit_torch import normalize_u8
+    g = golden("resvitkan_golden.npz")
+    crops = make_crops(4, seed=int(g["crop_seed"]))
+    m = rvk[dt]
+    lg_u8 = m.forward_u8(torch.from_numpy(crops).to(DEV))
+    lg_f32 = m(normalize_u8(crops).to(DEV))
+    torch.cuda.synchronize()
+    p_ref = 1 / (1 + np.exp(-g["logits"].astype(np.float64)))
+    for lg in (lg_u8, lg_f32):
+        p = 1 / (1 + np.exp(-lg.cpu().numpy().astype(np.float64)))
+        assert np.abs(p - p_ref).max() <= tol
+
+
+def test_resvitkan_features_match_emulation(rvk, golden):
+    """The ResNet-50 stem alone vs the oracle's emulation of the same 16-bit
+    rounding points (fp16): relative error of the [B,7,7,512] features."""
+    from oracle import resvitkan_torch as O
+    from oracle.cvit_torch import normalize_u8, to_torch_sd
+    from fac_fake_amd.ops import pack_input
+    g = golden("resvitkan_golden.npz")
+    x = normalize_u8(make_crops(2, seed=int(g["crop_seed"])))
+    m = rvk["fp16"]
+    f = m.features16(pack_input(x.to(DEV), dtype="fp16", u8=False, spatial=(224, 224)))
+    torch.cuda.synchronize()
+    ref = O.resnet50_emulated(to_torch_sd(make_resvitkan_state_dict(0)), x, "fp16").permute(0, 2, 3, 1)
+    err = (f.cpu().float().reshape(ref.shape) - ref).abs().max() / ref.abs().max()
+    assert err <= 5e-3
+
+
+def test_resvitkan_graph_replay_matches_eager(rvk):
+    m = rvk["bf16"]
+    crops = torch.from_numpy(make_crops(8, seed=5)).to(DEV)
+    eager = m.forward_u8(crops).clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        m.forward_u8(crops)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            out = m.forward_u8(crops)
+    gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)

@@ -11,7 +11,7 @@ REPO = Path(__file__).resolve().parents[1]
 
 
 def _header_symbols():
-    text = (REPO / "include" / "fac_cvit.h").read_text()
+    text = "".join(h.read_text() for h in sorted((REPO / "include").glob("*.h")))
     return sorted(set(re.findall(r"\b(fac_[a-z0-9_]+)\s*\(", text)))
 
 
