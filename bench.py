@@ -115,6 +115,56 @@ def video_measurement(model, dev, world: int, n_frames: int = 300, reps: int = 3
     return out
 
 
+RESVITKAN_FLOP_PER_CROP = 8.53e9   # conv + linear MACs x 2 of ResVitKan.py (KAN excluded)
+
+
+def resvitkan_measurement(dev, dtype: str, world: int, B: int = 256, steps: int = 10, warmup: int = 3,
+                          chunk: int | None = None):
+    """Config 5 (BASELINE.json configs[4]): ResVitKan forward (ResNet-50 stem
+    + CViT encoder + KAN head, fac_fake_amd/resvitkan.py) on B synthetic
+    uint8 crops resident in HBM, slot j mod 32, one hipGraph per step;
+    independent per rank (weak scaling), crops/s summed over ranks."""
+    from fac_fake_amd.resvitkan import ResVitKan
+    from fac_fake_amd.weights import make_resvitkan_state_dict
+    m = ResVitKan(dtype=dtype)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_resvitkan_state_dict(0).items()})
+    if chunk is not None:
+        m.feature_chunk = chunk
+    m.reserve(B, dev)
+    crops = torch.from_numpy(make_crops(B, seed=40 + int(os.environ.get("RANK", "0")))).to(dev)
+    pidx = (torch.arange(B, device=dev) % 32).to(torch.int32)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        m.forward_u8(crops, pos_index=pidx)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = m.forward_u8(crops, pos_index=pidx)
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    v = world * B * steps / el
+    peak = PEAK_TFLOPS[dtype]
+    assert torch.isfinite(out).all()
+    return {"workload": f"config 5: ResVitKan forward (ResNet-50 + CViT encoder + KAN head), B={B} crops per GPU, "
+                        "hipGraph per step", "value": round(v, 1), "unit": "face-crops/s", "n_gpus": world,
+            "ms_per_step": round(el / steps * 1e3, 3), "dtype": dtype,
+            "feature_chunk": m.feature_chunk,
+            "mfma_roofline_fraction": round(v * RESVITKAN_FLOP_PER_CROP / (world * peak * 1e12), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -130,6 +180,8 @@ def main():
     ap.add_argument("--no-fuse", action="store_true", help="unfused conv1..conv3 (A/B of the fused 224 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-video", action="store_true", help="skip the config-3 video sub-measurement")
+    ap.add_argument("--no-resvitkan", action="store_true", help="skip the config-5 ResVitKan sub-measurement")
+    ap.add_argument("--only", choices=["resvitkan"], help="run only one sub-measurement (profiling)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="fac_set_option knob (include/fac_cvit.h), repeatable")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
@@ -143,6 +195,12 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     B = args.batch
+    if args.only == "resvitkan":
+        r = resvitkan_measurement(dev, args.dtype, world, B, steps=args.steps, warmup=args.warmup,
+                                  chunk=args.stem_chunk if args.stem_chunk else None)
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+        return
 
     lib = _lib.load()
     sd = make_state_dict(0)
@@ -307,6 +365,8 @@ def main():
     }
     if not args.no_video:
         line["config3"] = video_measurement(model, dev, world)
+    if not args.no_resvitkan:
+        line["config5"] = resvitkan_measurement(dev, args.dtype, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(sd, threads)

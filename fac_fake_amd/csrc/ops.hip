@@ -13,11 +13,12 @@
 // steps of 32 (4 pieces of 8 channels).  The A tile is gathered on the fly
 // (im2col-free): every thread owns one GEMM row and two of its four pieces,
 // tracks its pieces' (channel piece, tap) incrementally (no divisions in the
-// K loop) and loads 16 bytes per piece, zero outside the input (padding) or
-// beyond the real K.  Operands are register-staged into a double-buffered LDS
-// image [piece][row] (16-byte entries: the 16 lanes of a ds_read_b128 group
-// read 16 consecutive entries, conflict-free), one barrier per K step, the
-// next step's global loads in flight during the current step's MFMAs.  The
+// K loop) and copies 16 bytes per piece, zero outside the input (padding) or
+// beyond the real K (a zero page).  Both operands go global -> LDS by
+// global_load_lds into a 4-slot ring of [piece][row] images (16-byte
+// entries: the 16 lanes of a ds_read_b128 group read 16 consecutive entries,
+// conflict-free), issued three K steps ahead with counted vmcnt waits, the
+// wait and the barrier in one asm statement (as in conv.hip).  The
 // epilogue stages the fp32 tile in LDS and writes 16-byte channel vectors
 // (bias, ReLU, residual, ReLU, convert), so a row's BN channels leave in one
 // contiguous burst.
@@ -61,19 +62,29 @@ __device__ __forceinline__ void trk_norm(Trk& t, int C8, int KH, int KW) {
   }
 }
 
-template <class T, int BN>
-__global__ __launch_bounds__(256, 2) void convnd_igemm(ConvP p) {
-  constexpr int BM = 128;
+// 16 zero bytes: the glds source of padding / out-of-range K pieces
+__device__ const uint16_t g_zero16[64] = {0};
+
+// Async global -> LDS copy of 16 bytes per lane (global_load_lds_dwordx4):
+// the wave's 64 pieces land contiguously at the wave-uniform LDS address.
+__device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
+}
+
+template <class T, int BM, int BN, int OCC>
+__global__ __launch_bounds__(256, OCC) void convnd_igemm(ConvP p) {
+  constexpr int BK = 64, NS = 3;
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int RT = WTM / 16, CT = WTN / 16;
-  constexpr int NBP = BN * 4 / 256;           // B pieces per thread per K step
+  constexpr int SLOT_A = BM * BK, SLOT = (BM + BN) * BK;  // u16 elements per ring slot
+  constexpr int NA = BM / 32, NB = BN / 32;               // glds per wave per stage (8 rows each)
+  constexpr int PER = NA + NB;
   constexpr int SPITCH = BN + 4;              // fp32 staging row pitch
-  constexpr int OPER = 2 * (4 * BM + 4 * BN) * 8;  // u16 elements, double-buffered
+  constexpr int OPER = NS * SLOT;
   constexpr int STG = BM * SPITCH * 2;        // u16 elements of the fp32 staging tile
   constexpr int SMEM = OPER > STG ? OPER : STG;
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
-  uint16_t* const sA = smem;                  // [2][4][BM][8]
-  uint16_t* const sB = smem + 2 * 4 * BM * 8;  // [2][4][BN][8]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -81,55 +92,54 @@ __global__ __launch_bounds__(256, 2) void convnd_igemm(ConvP p) {
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);  // XCD-contiguous row tiles
   const int m0 = bx * BM, n0 = blockIdx.y * BN;
 
-  // ---- A gather state: one row, pieces ja and ja + 2 of every K step
-  const int arow = tid & (BM - 1), ja = tid >> 7;
-  const int m = m0 + arow;
-  const bool mvalid = m < p.M;
-  int iz0, iy0, ix0;
-  const uint16_t* inb;
-  {
-    const int mm = mvalid ? m : 0;
+  // LDS images: rows of 64 k (128 B), the 16-byte piece j of row r at position
+  // j ^ ((r >> 1) & 7) (conflict-free ds_read_b128, as in transformer.hip's
+  // gemm_nt).  glds instruction i of this wave fills rows 8*(4i + wave) + lane/8,
+  // position lane % 8, so it copies piece j = (lane % 8) ^ ((row >> 1) & 7) —
+  // the same j for all of this lane's instructions, and 8 lanes cover one
+  // row's 128 contiguous bytes of K (coalesced when a K step stays in one tap).
+  const int pos = lane & 7, rsub = lane >> 3;
+  const int j = pos ^ ((4 * wave + (lane >> 4)) & 7);
+  // per A instruction: the output position of its row
+  const uint16_t* rbase[NA];
+  int riz[NA], riy[NA], rix[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + 8 * (4 * i + wave) + rsub;
+    const int mm = m < p.M ? m : 0;
     const int ox = mm % p.Wo, t1 = mm / p.Wo;
     const int oy = t1 % p.Ho, t2 = t1 / p.Ho;
     const int oz = t2 % p.Do, n = t2 / p.Do;
-    iz0 = oz * p.SD - p.PD;
-    iy0 = oy * p.SH - p.PH;
-    ix0 = ox * p.SW - p.PW;
-    inb = p.in + (size_t)n * p.D * p.H * p.W * p.C8 * 8;
+    riz[i] = m < p.M ? oz * p.SD - p.PD : -(1 << 29);  // rows past M: always out of range -> zeros
+    riy[i] = oy * p.SH - p.PH;
+    rix[i] = ox * p.SW - p.PW;
+    rbase[i] = p.in + (size_t)n * p.D * p.H * p.W * p.C8 * 8;
   }
-  Trk ta{ja, 0, 0, 0, ja}, tb{ja + 2, 0, 0, 0, ja + 2};
-  trk_norm(ta, p.C8, p.KH, p.KW);
-  trk_norm(tb, p.C8, p.KH, p.KW);
-  auto gather = [&](const Trk& t) -> u16x8 {
-    const int iz = iz0 + t.tz, iy = iy0 + t.ty, ix = ix0 + t.tx;
-    if (mvalid && t.kp < p.ktot8 && (unsigned)iz < (unsigned)p.D && (unsigned)iy < (unsigned)p.H &&
-        (unsigned)ix < (unsigned)p.W)
-      return *(const u16x8*)(inb + (((size_t)iz * p.H + iy) * p.W + ix) * p.C8 * 8 + t.c8 * 8);
-    return (u16x8)0;
-  };
-  auto advance = [&](Trk& t) {
-    t.kp += 4;
-    t.c8 += 4;
-    trk_norm(t, p.C8, p.KH, p.KW);
-  };
-  // ---- B (weights [cout_pad][Kp]): row brow, piece jb (+2 for BN = 128)
-  const int brow = tid % BN, jb = tid / BN;
-  const uint16_t* wrow = p.w + (size_t)(n0 + brow) * p.Kp;
+  // this lane's K piece (channel piece, tap), advanced 8 pieces per stage
+  Trk t{j, 0, 0, 0, j};
+  trk_norm(t, p.C8, p.KH, p.KW);
+  const uint16_t* wsrc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) wsrc[i] = p.w + (size_t)(n0 + 8 * (4 * i + wave) + rsub) * p.Kp + j * 8;
 
-  u16x8 ra0, ra1, rb[NBP];
-  auto load_step = [&](int s) {
-    ra0 = gather(ta);
-    ra1 = gather(tb);
+  // stage st -> ring slot st % NS; stages past the end copy zeros into slots never read
+  auto issue = [&](int st) {
+    uint16_t* slot = smem + (st % NS) * SLOT;
+    const bool real = st < p.ksteps && t.kp < p.ktot8;
 #pragma unroll
-    for (int i = 0; i < NBP; ++i) rb[i] = *(const u16x8*)(wrow + (size_t)(s * 4 + jb + i * (256 / BN)) * 8);
-  };
-  auto store_step = [&](int buf) {
-    uint16_t* a = sA + buf * 4 * BM * 8;
-    uint16_t* b = sB + buf * 4 * BN * 8;
-    *(u16x8*)(a + (ja * BM + arow) * 8) = ra0;
-    *(u16x8*)(a + ((ja + 2) * BM + arow) * 8) = ra1;
+    for (int i = 0; i < NA; ++i) {
+      const int iz = riz[i] + t.tz, iy = riy[i] + t.ty, ix = rix[i] + t.tx;
+      const bool ok = real && (unsigned)iz < (unsigned)p.D && (unsigned)iy < (unsigned)p.H &&
+                      (unsigned)ix < (unsigned)p.W;
+      const uint16_t* src = ok ? rbase[i] + (((size_t)iz * p.H + iy) * p.W + ix) * p.C8 * 8 + t.c8 * 8 : g_zero16;
+      glds16(src, slot + (4 * i + wave) * 64 * 8);
+    }
 #pragma unroll
-    for (int i = 0; i < NBP; ++i) *(u16x8*)(b + ((jb + i * (256 / BN)) * BN + brow) * 8) = rb[i];
+    for (int i = 0; i < NB; ++i)
+      glds16(st < p.ksteps ? wsrc[i] + (size_t)st * BK : g_zero16, slot + SLOT_A + (4 * i + wave) * 64 * 8);
+    t.kp += 8;
+    t.c8 += 8;
+    trk_norm(t, p.C8, p.KH, p.KW);
   };
 
   f32x4 acc[RT][CT];
@@ -138,32 +148,50 @@ __global__ __launch_bounds__(256, 2) void convnd_igemm(ConvP p) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = (f32x4)0.f;
 
-  load_step(0);
-  store_step(0);
-  __syncthreads();
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) issue(st);
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NS - 2) * PER) : "memory");
   for (int s = 0; s < p.ksteps; ++s) {
-    const bool more = s + 1 < p.ksteps;
-    if (more) {
-      advance(ta);
-      advance(tb);
-      load_step(s + 1);
+    issue(s + NS - 1);  // into the slot consumed at step s-1 (every wave passed its barrier)
+    const uint16_t* a = smem + (s % NS) * SLOT;
+    const uint16_t* b = a + SLOT_A;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+      u16x8 fb[CT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int r = wn * WTN + ct * 16 + (lane & 15);
+        fb[ct] = *(const u16x8*)(b + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = wm * WTM + rt * 16 + (lane & 15);
+        const u16x8 fa = *(const u16x8*)(a + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = T::mfma(fa, fb[ct], acc[rt][ct]);
+      }
     }
-    const uint16_t* a = sA + (s & 1) * 4 * BM * 8;
-    const uint16_t* b = sB + (s & 1) * 4 * BN * 8;
-    u16x8 fb[CT];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) fb[ct] = *(const u16x8*)(b + ((lane >> 4) * BN + wn * WTN + ct * 16 + (lane & 15)) * 8);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const u16x8 fa = *(const u16x8*)(a + ((lane >> 4) * BM + wm * WTM + rt * 16 + (lane & 15)) * 8);
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = T::mfma(fa, fb[ct], acc[rt][ct]);
-    }
-    if (more) store_step((s + 1) & 1);
-    __syncthreads();
+    // retire stage s+1 (stage s+2 stays in flight)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((NS - 2) * PER) : "memory");
   }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // dummy stages landed: LDS is free
 
-  // ---- epilogue: bias (+ReLU) in registers -> fp32 LDS tile -> 8-channel vectors
+  // ---- epilogue: bias (+ReLU) in registers -> fp32 LDS tile -> 8-channel
+  // vectors.  The residual's 16-byte vectors are loaded first, so their
+  // latency overlaps the staging.
+  constexpr int QPR = BN / 8;                 // 8-channel pieces per row
+  constexpr int QPT = BM * QPR / 256;         // pieces per thread
+  const bool resid = p.flags & FAC_CONV_RESID;
+  u16x8 rv[QPT];
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) {
+    const int q = tid + i * 256, row = q / QPR, cp = q - row * QPR;
+    const int mo = m0 + row, c = n0 + cp * 8;
+    rv[i] = (u16x8)0;
+    if (resid && p.vec_res && mo < p.M && c + 8 <= p.Cout)
+      rv[i] = *(const u16x8*)(p.res + (size_t)mo * p.ldr + p.r_off + c);
+  }
   float* stg = (float*)smem;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
@@ -179,33 +207,31 @@ __global__ __launch_bounds__(256, 2) void convnd_igemm(ConvP p) {
       }
   }
   __syncthreads();
-  constexpr int QPR = BN / 8;  // 8-channel pieces per row
-#pragma unroll 2
-  for (int q = tid; q < BM * QPR; q += 256) {
-    const int row = q / QPR, cp = q - row * QPR;
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) {
+    const int q = tid + i * 256, row = q / QPR, cp = q - row * QPR;
     const int mo = m0 + row, c = n0 + cp * 8;
     if (mo >= p.M || c >= p.Cout) continue;
     const int nc = min(8, p.Cout - c);
     const f32x4 lo = *(const f32x4*)(stg + row * SPITCH + cp * 8);
     const f32x4 hi = *(const f32x4*)(stg + row * SPITCH + cp * 8 + 4);
     float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    if (p.flags & FAC_CONV_RESID) {
-      const uint16_t* r = p.res + (size_t)mo * p.ldr + p.r_off + c;
+    if (resid) {
       if (p.vec_res && nc == 8) {
-        const u16x8 rv = *(const u16x8*)r;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += T::to_f32(rv[i]);
+        for (int k = 0; k < 8; ++k) v[k] += T::to_f32(rv[i][k]);
       } else {
-        for (int i = 0; i < nc; ++i) v[i] += T::to_f32(r[i]);
+        const uint16_t* r = p.res + (size_t)mo * p.ldr + p.r_off + c;
+        for (int k = 0; k < nc; ++k) v[k] += T::to_f32(r[k]);
       }
     }
     if (p.flags & FAC_CONV_RELU2) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = relu(v[i]);
+      for (int k = 0; k < 8; ++k) v[k] = relu(v[k]);
     }
     if (p.flags & FAC_CONV_OUT_F32) {
       float* o = (float*)p.out + (size_t)mo * p.ldo + p.c_off + c;
-      for (int i = 0; i < nc; ++i) o[i] = v[i];
+      for (int k = 0; k < nc; ++k) o[k] = v[k];
     } else {
       uint16_t* o = (uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c;
       if (p.vec_out && nc == 8) {
@@ -213,7 +239,7 @@ __global__ __launch_bounds__(256, 2) void convnd_igemm(ConvP p) {
         const u16x4 b = T::pack4((f32x4){v[4], v[5], v[6], v[7]});
         *(u16x8*)o = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
       } else {
-        for (int i = 0; i < nc; ++i) o[i] = T::from_f32(v[i]);
+        for (int k = 0; k < nc; ++k) o[k] = T::from_f32(v[k]);
       }
     }
   }
@@ -367,11 +393,10 @@ __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, fl
 template <class T>
 static hipError_t launch_convnd(const ConvP& p, int cout_pad, hipStream_t st) {
   const int gx = (p.M + 127) / 128;
-  if (cout_pad % 128 == 0 && p.Cout > 64) {
-    convnd_igemm<T, 128><<<dim3(gx, cout_pad / 128), 256, 0, st>>>(p);
-  } else {
-    convnd_igemm<T, 64><<<dim3(gx, (p.Cout + 63) / 64), 256, 0, st>>>(p);
-  }
+  // 128 x 64 tiles, two workgroups per CU (72 KB ring each): measured faster
+  // than 128 x 128 at one per CU on every ResNet-50 layer (tools/rvk_layers.py)
+  (void)cout_pad;
+  convnd_igemm<T, 128, 64, 2><<<dim3(gx, (p.Cout + 63) / 64), 256, 0, st>>>(p);
   return hipGetLastError();
 }
 
@@ -382,7 +407,7 @@ extern "C" {
 int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad) {
   if (cout <= 0 || cin <= 0 || kd <= 0 || kh <= 0 || kw <= 0 || !cout_pad || !k_pad) return FAC_ERR_ARG;
   *cout_pad = (cout + 127) / 128 * 128;
-  *k_pad = (kd * kh * kw * cin + 31) / 32 * 32;
+  *k_pad = (kd * kh * kw * cin + 63) / 64 * 64;
   return FAC_OK;
 }
 
@@ -429,7 +454,7 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   p.PH = d->ph;
   p.PW = d->pw;
   p.Kp = k_pad;
-  p.ksteps = k_pad / 32;
+  p.ksteps = k_pad / 64;
   p.ktot8 = d->kd * d->kh * d->kw * (d->cin / 8);
   p.ldo = d->ldo;
   p.c_off = d->c_off;

@@ -176,16 +176,29 @@ class ResVitKan(nn.Module):
         _lib.check(_lib.load().fac_reserve(self._ctx, int(max_batch)), self._ctx, "fac_reserve")
 
     # ------------------------------------------------------------------ forward
-    def features16(self, x16: torch.Tensor) -> torch.Tensor:
+    # crops per pass of the ResNet stem (0 = the whole batch).  Smaller chunks
+    # keep a block's activations in the Infinity Cache, but measured on MI355X
+    # (B = 256, bf16) the whole batch is fastest: 8.9 ms vs 9.5 / 11.0 / 15.6
+    # ms at 128 / 64 / 32 — the layers are not HBM-bound, the smaller grids
+    # just fill the 256 CUs worse (tools/rvk_chunks.sh)
+    feature_chunk = 0
+
+    def features16(self, x16: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """ResNet.forward (ResVitKan.py:232-247) on packed 16-bit [B,1,224,224,8]
-        -> [B,1,7,7,512] 16-bit NHWC."""
-        x = self._conv1(x16)                                        # 7x7/2 + bn1 + ReLU
-        x = pool(x, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")         # MaxPool2d(3, 2, 1)
-        for c1, c2, c3, ds in self._blocks:
-            res = ds(x, relu=False) if ds is not None else x
-            h = c2(c1(x))
-            x = c3(h, residual=res, relu2=True)                     # relu(bn3) + residual, relu
-        return self._channel(x, relu=False)                         # channel 1x1 + bn2
+        -> [B,1,7,7,512] 16-bit NHWC, in chunks of ``feature_chunk`` crops."""
+        B = x16.shape[0]
+        if out is None:
+            out = torch.empty(B, 1, 7, 7, 512, dtype=x16.dtype, device=x16.device)
+        step = self.feature_chunk or B
+        for b0 in range(0, B, step):
+            x = self._conv1(x16[b0:b0 + step])                      # 7x7/2 + bn1 + ReLU
+            x = pool(x, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")     # MaxPool2d(3, 2, 1)
+            for c1, c2, c3, ds in self._blocks:
+                res = ds(x, relu=False) if ds is not None else x
+                h = c2(c1(x))
+                x = c3(h, residual=res, relu2=True)                 # relu(bn3) + residual, relu
+            self._channel(x, relu=False, out=out[b0:b0 + step])     # channel 1x1 + bn2
+        return out
 
     def _run(self, x16: torch.Tensor, pos_index, want_probs: bool):
         B = x16.shape[0]
@@ -232,7 +245,8 @@ def _pos_index(B: int, pos_index, device) -> torch.Tensor:
     p = torch.as_tensor(pos_index)
     if p.shape != (B,):
         raise ValueError(f"pos_index must have shape ({B},), got {tuple(p.shape)}")
-    if p.numel() and (int(p.min()) < 0 or int(p.max()) >= MAX_SLOTS):
+    # (a device tensor is range-checked eagerly, not while a hipGraph is being captured)
+    if p.numel() and not torch.cuda.is_current_stream_capturing() and (int(p.min()) < 0 or int(p.max()) >= MAX_SLOTS):
         raise IndexError(f"pos_index values must lie in [0, {MAX_SLOTS})")
     return p.to(device=device, dtype=torch.int32).contiguous()
 

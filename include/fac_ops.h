@@ -41,7 +41,7 @@ extern "C" {
  *
  * weight: 16-bit [cout_pad][k_pad], row o = output channel, k index =
  *   ((tz*kh + ty)*kw + tx)*cin + c, zero beyond taps*cin; cout_pad a
- *   multiple of 128, k_pad a multiple of 32 (fac_conv_weight_layout).
+ *   multiple of 128, k_pad a multiple of 64 (fac_conv_weight_layout).
  * bias: fp32 [cout_pad] (BN shift folded in).
  * out: row m = ((n*Do + z)*Ho + y)*Wo + x, element [m*ldo + c_off + c];
  *   c_off lets Inception branches write straight into their concat slot.
@@ -67,7 +67,7 @@ typedef struct fac_conv_desc {
 int fac_conv_nd(const fac_conv_desc* desc, void* stream);
 
 /* Weight packing geometry for fac_conv_nd: *cout_pad = cout rounded up to
- * 128, *k_pad = taps*cin rounded up to 32. */
+ * 128, *k_pad = taps*cin rounded up to 64. */
 int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad);
 
 /* Max or average pooling, channels-last 16-bit (MaxPool2d/3d: padding is
