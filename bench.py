@@ -165,6 +165,48 @@ def resvitkan_measurement(dev, dtype: str, world: int, B: int = 256, steps: int 
             "mfma_roofline_fraction": round(v * RESVITKAN_FLOP_PER_CROP / (world * peak * 1e12), 4)}
 
 
+S3D_FLOP_PER_CLIP = 8.95e9   # per 16x112x112 clip (Conv3d hooks over S3D/model.py)
+
+
+def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, warmup: int = 3, srm: str = "no"):
+    """Config 4 (BASELINE.json configs[3]): S3D forward (fac_fake_amd/s3d.py) on
+    B synthetic raw 16x112x112 clips resident in HBM, one hipGraph per step;
+    independent per rank (weak scaling), clips/s summed over ranks."""
+    from fac_fake_amd.s3d import S3D
+    from fac_fake_amd.weights import make_s3d_state_dict, s3d_clips
+    m = S3D(1, srm, dtype=dtype)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, srm == "yes").items()})
+    x = torch.from_numpy(s3d_clips(B, 16, 112, seed=50 + int(os.environ.get("RANK", "0")))).to(dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        m(x)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = m(x)
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    v = world * B * steps / el
+    assert torch.isfinite(out).all()
+    return {"workload": f"config 4: S3D forward (SRM_net={srm}), B={B} raw 16x112x112 clips per GPU, hipGraph per step",
+            "value": round(v, 1), "unit": "clips/s", "n_gpus": world, "ms_per_step": round(el / steps * 1e3, 3),
+            "dtype": dtype,
+            "mfma_roofline_fraction": round(v * S3D_FLOP_PER_CLIP / (world * PEAK_TFLOPS[dtype] * 1e12), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -181,7 +223,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-video", action="store_true", help="skip the config-3 video sub-measurement")
     ap.add_argument("--no-resvitkan", action="store_true", help="skip the config-5 ResVitKan sub-measurement")
-    ap.add_argument("--only", choices=["resvitkan"], help="run only one sub-measurement (profiling)")
+    ap.add_argument("--no-s3d", action="store_true", help="skip the config-4 S3D sub-measurement")
+    ap.add_argument("--only", choices=["resvitkan", "s3d"], help="run only one sub-measurement (profiling)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="fac_set_option knob (include/fac_cvit.h), repeatable")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
@@ -198,6 +241,11 @@ def main():
     if args.only == "resvitkan":
         r = resvitkan_measurement(dev, args.dtype, world, B, steps=args.steps, warmup=args.warmup,
                                   chunk=args.stem_chunk if args.stem_chunk else None)
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+        return
+    if args.only == "s3d":
+        r = s3d_measurement(dev, args.dtype, world, steps=args.steps, warmup=args.warmup)
         if rank == 0:
             print(json.dumps(r), flush=True)
         return
@@ -365,6 +413,8 @@ def main():
     }
     if not args.no_video:
         line["config3"] = video_measurement(model, dev, world)
+    if not args.no_s3d:
+        line["config4"] = s3d_measurement(dev, args.dtype, world)
     if not args.no_resvitkan:
         line["config5"] = resvitkan_measurement(dev, args.dtype, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,178 @@
+"""Drop-in ``S3D`` (BASELINE config 4) on gfx950 HIP kernels.
+
+Mirrors ``sx_exp_deepfakedetect-master/S3D/model.py::S3D`` (:6-48): the same
+constructor ``S3D(num_class, SRM_net)``, the same 465-key ``state_dict``
+(``SRM.hpf``, ``base.{0..15}`` with BasicConv3d / SepConv3d / Mixed_* blocks,
+``fc.0``) and ``forward(x)`` on a raw clip ``[B, 3, T, H, W]`` (0..255 BGR
+floats, un-normalised — S3D-test.py:94-96) returning logits ``[B, num_class]``.
+
+Arithmetic (every layer a HIP kernel of libfac_cvit.so, no CPU fallback):
+
+* each Conv3d + BatchNorm3d(eval, eps 1e-3) + ReLU is one ``fac_conv_nd``
+  implicit-GEMM launch with the BN folded on the host; SepConv3d is its
+  (1,k,k) spatial and (k,1,1) temporal convs; the Inception branches write
+  straight into their channel slot of the block output (no concat copy);
+* MaxPool3d / the final avg_pool3d are ``fac_pool_nd``;
+* the SRM high-pass bank (``SRM_net == 'yes'``, SRM/HPF.py) is a 3 -> 30
+  (1,5,5) conv without BN or ReLU, written into a 32-channel buffer;
+* ``fc`` (1x1x1 conv with bias) writes fp32 logits.  ``avg_pool3d((2, H, W),
+  stride=1)`` then ``torch.mean`` over time is evaluated as two average pools
+  before ``fc`` (identical in exact arithmetic: fc is affine).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from . import _lib
+from .cvit import _Node
+from .ops import TORCH16, ConvLayer, fold_bn, pack_input, pool, sigmoid
+from .weights import s3d_base, s3d_param_specs
+
+BN_EPS = 1e-3   # BatchNorm3d(eps=1e-3) in BasicConv3d / SepConv3d (model.py:54,67,71)
+_BUFFERS = ("rmean", "rvar", "nbt")
+
+
+def _init_tensor(shape, kind):
+    if kind == "nbt":
+        return torch.zeros((), dtype=torch.long)
+    if kind in ("rmean", "beta", "lbias"):
+        return torch.zeros(shape)
+    if kind in ("rvar", "gamma"):
+        return torch.ones(shape)
+    t = torch.empty(shape)
+    bound = 1.0 / math.sqrt(int(math.prod(shape[1:])))
+    return t.uniform_(-bound, bound)
+
+
+class S3D(nn.Module):
+    def __init__(self, num_class: int, SRM_net: str, *, dtype: str = "bf16"):
+        super().__init__()
+        if dtype not in _lib.DTYPES:
+            raise ValueError(f"dtype must be one of {list(_lib.DTYPES)}")
+        self.num_class = num_class
+        self.SRM_net = SRM_net
+        self.dtype_name = dtype
+        self._srm = SRM_net == "yes"
+        for name, shape, kind in s3d_param_specs(num_class, self._srm):
+            *path, leaf = name.split(".")
+            mod = self
+            for p in path:
+                if p not in mod._modules:
+                    mod.add_module(p, _Node())
+                mod = mod._modules[p]
+            t = _init_tensor(shape, kind)
+            if kind in _BUFFERS:
+                mod.register_buffer(leaf, t)
+            else:
+                mod.register_parameter(leaf, nn.Parameter(t))
+        self._prep = None
+        self.eval()
+
+    def _versions(self):
+        return tuple(t._version for t in self.state_dict(keep_vars=True).values()) + (
+            tuple(t.data_ptr() for t in self.parameters()),)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        out = super().load_state_dict(state_dict, strict=strict, assign=assign)
+        self._prep = None
+        return out
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise RuntimeError("the gfx950 S3D path is inference-only (BatchNorm is folded into the convs)")
+        return super().train(False)
+
+    # ------------------------------------------------------------------ weights
+    def _prepare(self, device: torch.device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        v = self._versions()
+        if self._prep == (idx, v):
+            return
+        sd = self.state_dict()
+        dt = self.dtype_name
+
+        def bconv(p, stride=1, pad=0, cin_pad=None, kind="basic"):
+            ck, bn = (f"{p}.conv", f"{p}.bn") if kind == "basic" else (f"{p}.conv_{kind}", f"{p}.bn_{kind}")
+            w, b = fold_bn(sd[ck + ".weight"], None, sd[bn + ".weight"], sd[bn + ".bias"], sd[bn + ".running_mean"],
+                           sd[bn + ".running_var"], BN_EPS)
+            return ConvLayer(w, b, stride, pad, dtype=dt, device=device, cin_pad=cin_pad)
+
+        def sep(p, k, s, pd, cin_pad=None):
+            return (bconv(p, (1, s, s), (0, pd, pd), cin_pad, "s"), bconv(p, (s, 1, 1), (pd, 0, 0), None, "t"))
+
+        self._srm_conv = None
+        if self._srm:
+            w = sd["SRM.hpf.weight"]
+            self._srm_conv = ConvLayer(w, torch.zeros(w.shape[0]), 1, (0, 2, 2), dtype=dt, device=device)
+        self._layers = []
+        for i, L in enumerate(s3d_base(self._srm)):
+            p = f"base.{i}"
+            if L[0] == "sep":
+                self._layers.append(("sep", sep(p, L[3], L[4], L[5], cin_pad=32 if (i == 0 and self._srm) else None)))
+            elif L[0] == "basic":
+                self._layers.append(("basic", bconv(p)))
+            elif L[0] == "pool":
+                self._layers.append(("pool", L[1:]))
+            else:
+                cin, b0, (b1a, b1b), (b2a, b2b), b3 = L[1:]
+                self._layers.append(("mixed", dict(
+                    b0=bconv(f"{p}.branch0.0"), b1a=bconv(f"{p}.branch1.0"), b1=sep(f"{p}.branch1.1", 3, 1, 1),
+                    b2a=bconv(f"{p}.branch2.0"), b2=sep(f"{p}.branch2.1", 3, 1, 1), b3=bconv(f"{p}.branch3.1"),
+                    widths=(b0, b1b, b2b, b3))))
+        self._fc = ConvLayer(sd["fc.0.weight"], sd["fc.0.bias"], 1, 0, dtype=dt, device=device)
+        self._prep = (idx, v)
+
+    # ------------------------------------------------------------------ forward
+    @staticmethod
+    def _mixed(x, blk):
+        n, d, h, w, _ = x.shape
+        out = torch.empty(n, d, h, w, sum(blk["widths"]), dtype=x.dtype, device=x.device)
+        o1 = blk["widths"][0]
+        o2 = o1 + blk["widths"][1]
+        o3 = o2 + blk["widths"][2]
+        blk["b0"](x, out=out, c_off=0)
+        s1, t1 = blk["b1"]
+        t1(s1(blk["b1a"](x)), out=out, c_off=o1)
+        s2, t2 = blk["b2"]
+        t2(s2(blk["b2a"](x)), out=out, c_off=o2)
+        blk["b3"](pool(x, 3, 1, 1, "max"), out=out, c_off=o3)        # MaxPool3d(3, 1, 1) then 1x1x1
+        return out
+
+    def features16(self, x16: torch.Tensor) -> torch.Tensor:
+        """`base` (model.py:17-33) on the packed clip -> [B, T', H', W', 1024] 16-bit."""
+        y = x16
+        if self._srm_conv is not None:
+            n, d, h, w, _ = y.shape
+            s = torch.zeros(n, d, h, w, 32, dtype=y.dtype, device=y.device)   # 30 filters + 2 zero channels
+            y = self._srm_conv(y, relu=False, out=s)
+        for kind, L in self._layers:
+            if kind == "sep":
+                y = L[1](L[0](y))
+            elif kind == "basic":
+                y = L(y)
+            elif kind == "pool":
+                y = pool(y, *L, mode="max")
+            else:
+                y = self._mixed(y, L)
+        return y
+
+    def forward(self, x: torch.Tensor, return_probs: bool = False):
+        if not x.is_cuda:
+            raise RuntimeError("S3D (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
+        if x.dim() != 5 or x.shape[1] != 3:
+            raise ValueError(f"expected a clip [B,3,T,H,W], got {tuple(x.shape)}")
+        self._prepare(x.device)
+        B, _, T, H, W = x.shape
+        x16 = pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
+        y = self.features16(x16)
+        _, t, h, w, _ = y.shape
+        y = pool(y, (2, h, w), 1, 0, "avg")                           # F.avg_pool3d(y, (2, H, W), stride=1)
+        y = pool(y, (y.shape[1], 1, 1), 1, 0, "avg")                  # torch.mean over time (before fc: affine)
+        logits = self._fc(y, relu=False, out_f32=True).view(B, self.num_class)
+        return (logits, sigmoid(logits)) if return_probs else logits
+
+
+__all__ = ["S3D", "TORCH16"]

@@ -267,3 +267,112 @@ def _synthetic(name, shape, kind, seed):
               "beta": (-0.1, 0.1), "rmean": (-0.1, 0.1), "rvar": (0.8, 1.2)}
     lo, hi = ranges[kind]
     return _u(name, shape, seed, lo, hi)
+
+
+# ---------------------------------------------------------------- S3D
+# sx_exp_deepfakedetect-master/S3D/model.py: S3D(num_class, SRM_net) (:6-48)
+# with BasicConv3d / SepConv3d (:50-82, BatchNorm3d eps 1e-3) and the
+# Mixed_* Inception blocks (:84-342).  Each entry of S3D_BASE is one
+# nn.Sequential index of `base`:
+#   ("sep", cin, cout, k, stride, pad) | ("basic", cin, cout) | ("pool", k, s, p)
+#   | ("mixed", cin, b0, (b1a, b1b), (b2a, b2b), b3)
+S3D_MIXED = {
+    5: (192, 64, (96, 128), (16, 32), 32), 6: (256, 128, (128, 192), (32, 96), 64),
+    8: (480, 192, (96, 208), (16, 48), 64), 9: (512, 160, (112, 224), (24, 64), 64),
+    10: (512, 128, (128, 256), (24, 64), 64), 11: (512, 112, (144, 288), (32, 64), 64),
+    12: (528, 256, (160, 320), (32, 128), 128), 14: (832, 256, (160, 320), (32, 128), 128),
+    15: (832, 384, (192, 384), (48, 128), 128)}
+S3D_POOLS = {1: ((1, 3, 3), (1, 2, 2), (0, 1, 1)), 4: ((1, 3, 3), (1, 2, 2), (0, 1, 1)),
+             7: ((3, 3, 3), (2, 2, 2), (1, 1, 1)), 13: ((2, 2, 2), (2, 2, 2), (0, 0, 0))}
+
+
+def s3d_base(srm: bool):
+    """The `base` Sequential of S3D (model.py:17-33) as layer descriptors."""
+    cin = 30 if srm else 3
+    out = []
+    for i in range(16):
+        if i == 0:
+            out.append(("sep", cin, 64, 7, 2, 3))
+        elif i == 2:
+            out.append(("basic", 64, 64))
+        elif i == 3:
+            out.append(("sep", 64, 192, 3, 1, 1))
+        elif i in S3D_POOLS:
+            out.append(("pool",) + S3D_POOLS[i])
+        else:
+            out.append(("mixed",) + S3D_MIXED[i])
+    return out
+
+
+def _s3d_bn(p, c):
+    return [(f"{p}.weight", (c,), "gamma"), (f"{p}.bias", (c,), "beta"), (f"{p}.running_mean", (c,), "rmean"),
+            (f"{p}.running_var", (c,), "rvar"), (f"{p}.num_batches_tracked", (), "nbt")]
+
+
+def _s3d_basic(p, cin, cout):
+    return [(f"{p}.conv.weight", (cout, cin, 1, 1, 1), "conv")] + _s3d_bn(f"{p}.bn", cout)
+
+
+def _s3d_sep(p, cin, cout, k):
+    return ([(f"{p}.conv_s.weight", (cout, cin, 1, k, k), "conv")] + _s3d_bn(f"{p}.bn_s", cout) +
+            [(f"{p}.conv_t.weight", (cout, cout, k, 1, 1), "conv")] + _s3d_bn(f"{p}.bn_t", cout))
+
+
+def s3d_param_specs(num_class: int = 1, srm: bool = False):
+    """(name, shape, kind) for every key of S3D's state_dict, in its order."""
+    specs = [("SRM.hpf.weight", (30, 3, 1, 5, 5), "srm")]
+    for i, L in enumerate(s3d_base(srm)):
+        p = f"base.{i}"
+        if L[0] == "sep":
+            specs += _s3d_sep(p, L[1], L[2], L[3])
+        elif L[0] == "basic":
+            specs += _s3d_basic(p, L[1], L[2])
+        elif L[0] == "mixed":
+            cin, b0, (b1a, b1b), (b2a, b2b), b3 = L[1:]
+            specs += _s3d_basic(f"{p}.branch0.0", cin, b0)
+            specs += _s3d_basic(f"{p}.branch1.0", cin, b1a) + _s3d_sep(f"{p}.branch1.1", b1a, b1b, 3)
+            specs += _s3d_basic(f"{p}.branch2.0", cin, b2a) + _s3d_sep(f"{p}.branch2.1", b2a, b2b, 3)
+            specs += _s3d_basic(f"{p}.branch3.1", cin, b3)
+    specs += [("fc.0.weight", (num_class, 1024, 1, 1, 1), "fc"), ("fc.0.bias", (num_class,), "lbias")]
+    return specs
+
+
+def make_s3d_state_dict(seed: int = 0, num_class: int = 1, srm: bool = False) -> "OrderedDict[str, np.ndarray]":
+    """Synthetic S3D weights (same scheme as make_state_dict).  Inputs are raw
+    0..255 pixels (S3D-test.py:94-96 feeds un-normalised clips), so BN running
+    means/vars of the first layer are scaled to that range; the SRM filters
+    are zero-sum 5x5 high-pass kernels like the reference bank's."""
+    sd = OrderedDict()
+    for name, shape, kind in s3d_param_specs(num_class, srm):
+        if kind == "nbt":
+            sd[name] = np.array(0, dtype=np.int64)
+        elif kind == "conv":
+            fan_in = int(np.prod(shape[1:]))
+            a = float(np.sqrt(6.0 / fan_in))
+            sd[name] = _u(name, shape, seed, -a, a)
+        elif kind == "srm":
+            w = _u(name, shape, seed, -0.25, 0.25)
+            w = w - w.mean(axis=(3, 4), keepdims=True)   # high-pass: each 5x5 kernel sums to 0
+            sd[name] = w.astype(np.float32)
+        elif kind == "fc":
+            a = float(4.0 / np.sqrt(shape[1]))
+            sd[name] = _u(name, shape, seed, -a, a)
+        elif name.startswith("base.0.bn_s.") and kind in ("rmean", "rvar"):
+            # first conv sees 0..255 pixels (or SRM residuals of them): BN statistics on that scale
+            lo, hi = ((-40.0, 40.0) if kind == "rmean" else (2.0e4, 6.0e4)) if not srm else \
+                ((-2.0, 2.0) if kind == "rmean" else (8.0e3, 2.4e4))
+            sd[name] = _u(name, shape, seed, lo, hi)
+        elif kind == "gamma":
+            # ReLU'd activations feed BNs whose synthetic running means are ~0: keep the
+            # ~30-layer stack from growing by shrinking every BN scale
+            sd[name] = _u(name, shape, seed, 0.8, 1.0)
+        else:
+            sd[name] = _synthetic(name, shape, kind, seed)
+    return sd
+
+
+def s3d_clips(n: int, frames: int, size: int, seed: int) -> np.ndarray:
+    """n synthetic raw clips [n, 3, frames, size, size] float32 of integer pixel
+    values 0..255 (S3D's un-normalised BGR input, S3D-test.py:94-96)."""
+    z = splitmix64(np.arange(n * 3 * frames * size * size, dtype=np.uint64), _stream_seed(seed, "clips"))
+    return (z >> np.uint64(56)).astype(np.float32).reshape(n, 3, frames, size, size)

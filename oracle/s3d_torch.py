@@ -1,0 +1,122 @@
+"""ORACLE (test infrastructure, never shipped or measured as the product).
+
+CPU restatement of the S3D clip classifier (BASELINE config 4,
+``sx_exp_deepfakedetect-master/S3D/model.py``), functional over a state_dict
+with the PyTorch CPU ops the reference modules call:
+
+* ``forward_fp32``     - ``S3D.forward`` (model.py:37-48): optional SRM
+                         high-pass conv (SRM/HPF.py:11-37), ``base`` (SepConv3d
+                         = (1,k,k) + (k,1,1) convs, BasicConv3d, Mixed_*
+                         Inception blocks with their channel concat, MaxPool3d),
+                         ``avg_pool3d((2, H, W), stride=1)``, ``fc``, mean over
+                         time.  Pinned against the reference module's outputs
+                         (tests/golden/s3d_*, tools/make_golden_s3d.py).
+* ``forward_emulated`` - the gfx950 path's rounding points: 16-bit input,
+                         BN-folded 16-bit weights, every conv / pool output
+                         rounded to 16 bits, fp32 accumulation and fc output;
+                         the time mean taken before fc (fc is affine).
+
+Only tests/, __graft_entry__.smoke() and bench.py may import this package.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from fac_fake_amd.weights import s3d_base
+
+from .cvit_torch import round_to, to_torch_sd
+
+BN_EPS = 1e-3
+
+
+def _bn(sd, p, x):
+    return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"], sd[p + ".bias"],
+                        False, 0.001, BN_EPS)
+
+
+def _basic(sd, p, x, conv=None):
+    return F.relu(_bn(sd, p + ".bn", F.conv3d(x, sd[p + ".conv.weight"])))
+
+
+def _sep(sd, p, x, k, s, pd):
+    x = F.relu(_bn(sd, p + ".bn_s", F.conv3d(x, sd[p + ".conv_s.weight"], stride=(1, s, s), padding=(0, pd, pd))))
+    return F.relu(_bn(sd, p + ".bn_t", F.conv3d(x, sd[p + ".conv_t.weight"], stride=(s, 1, 1), padding=(pd, 0, 0))))
+
+
+@torch.no_grad()
+def features_fp32(sd, x: torch.Tensor, srm: bool) -> torch.Tensor:
+    sd = to_torch_sd(sd)
+    y = F.conv3d(x.float(), sd["SRM.hpf.weight"], padding=(0, 2, 2)) if srm else x.float()
+    for i, L in enumerate(s3d_base(srm)):
+        p = f"base.{i}"
+        if L[0] == "sep":
+            y = _sep(sd, p, y, L[3], L[4], L[5])
+        elif L[0] == "basic":
+            y = _basic(sd, p, y)
+        elif L[0] == "pool":
+            y = F.max_pool3d(y, *L[1:])
+        else:
+            y0 = _basic(sd, f"{p}.branch0.0", y)
+            y1 = _sep(sd, f"{p}.branch1.1", _basic(sd, f"{p}.branch1.0", y), 3, 1, 1)
+            y2 = _sep(sd, f"{p}.branch2.1", _basic(sd, f"{p}.branch2.0", y), 3, 1, 1)
+            y3 = _basic(sd, f"{p}.branch3.1", F.max_pool3d(y, 3, 1, 1))
+            y = torch.cat((y0, y1, y2, y3), 1)
+    return y
+
+
+@torch.no_grad()
+def forward_fp32(sd, x: torch.Tensor, srm: bool) -> torch.Tensor:
+    """S3D.forward (model.py:37-48)."""
+    sd = to_torch_sd(sd)
+    y = features_fp32(sd, x, srm)
+    y = F.avg_pool3d(y, (2, y.size(3), y.size(4)), stride=1)
+    y = F.conv3d(y, sd["fc.0.weight"], sd["fc.0.bias"])
+    y = y.view(y.size(0), y.size(1), y.size(2))
+    return torch.mean(y, 2)
+
+
+def _fold(sd, ck, bn):
+    s = sd[bn + ".weight"] / torch.sqrt(sd[bn + ".running_var"] + torch.tensor(BN_EPS))
+    w = sd[ck] * s.view(-1, 1, 1, 1, 1)
+    b = (torch.zeros_like(s) - sd[bn + ".running_mean"]) * s + sd[bn + ".bias"]
+    return w, b
+
+
+@torch.no_grad()
+def forward_emulated(sd, x: torch.Tensor, srm: bool, dtype: str = "bf16") -> torch.Tensor:
+    sd = to_torch_sd(sd)
+    r = lambda t: round_to(t, dtype)  # noqa: E731
+
+    def conv(y, ck, bn, stride=1, pad=0):
+        w, b = _fold(sd, ck, bn)
+        return r(F.relu(F.conv3d(y, r(w), b, stride=stride, padding=pad)))
+
+    def basic(p, y):
+        return conv(y, p + ".conv.weight", p + ".bn")
+
+    def sep(p, y, k, s, pd):
+        y = conv(y, p + ".conv_s.weight", p + ".bn_s", (1, s, s), (0, pd, pd))
+        return conv(y, p + ".conv_t.weight", p + ".bn_t", (s, 1, 1), (pd, 0, 0))
+
+    y = r(x.float())
+    if srm:
+        y = r(F.conv3d(y, r(sd["SRM.hpf.weight"]), padding=(0, 2, 2)))
+    for i, L in enumerate(s3d_base(srm)):
+        p = f"base.{i}"
+        if L[0] == "sep":
+            y = sep(p, y, L[3], L[4], L[5])
+        elif L[0] == "basic":
+            y = basic(p, y)
+        elif L[0] == "pool":
+            y = F.max_pool3d(y, *L[1:])
+        else:
+            y0 = basic(f"{p}.branch0.0", y)
+            y1 = sep(f"{p}.branch1.1", basic(f"{p}.branch1.0", y), 3, 1, 1)
+            y2 = sep(f"{p}.branch2.1", basic(f"{p}.branch2.0", y), 3, 1, 1)
+            y3 = basic(f"{p}.branch3.1", F.max_pool3d(y, 3, 1, 1))
+            y = torch.cat((y0, y1, y2, y3), 1)
+    y = r(F.avg_pool3d(y, (2, y.size(3), y.size(4)), stride=1))
+    y = r(y.mean(2, keepdim=True))
+    y = F.conv3d(y, r(sd["fc.0.weight"]), sd["fc.0.bias"])
+    return y.view(y.size(0), y.size(1))

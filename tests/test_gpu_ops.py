@@ -191,3 +191,62 @@ def test_resvitkan_graph_replay_matches_eager(rvk):
     gr.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, eager)
+
+
+# ---------------------------------------------------------------- S3D (config 4)
+@pytest.fixture(scope="module")
+def s3d_models():
+    from fac_fake_amd.s3d import S3D
+    from fac_fake_amd.weights import make_s3d_state_dict
+    out = {}
+    for srm in ("no", "yes"):
+        sd = {k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, srm == "yes").items()}
+        for dt in ("fp16", "bf16"):
+            m = S3D(1, srm, dtype=dt)
+            m.load_state_dict(sd)
+            out[(srm, dt)] = m
+    return out
+
+
+@pytest.mark.parametrize("srm", ["no", "yes"])
+@pytest.mark.parametrize("dt,tol", [("fp16", 1e-3), ("bf16", 1e-2)])
+def test_s3d_matches_reference(s3d_models, golden, srm, dt, tol):
+    """Per-logit sigmoid of 2 raw 16x112x112 clips vs the reference module (golden)."""
+    from fac_fake_amd.weights import s3d_clips
+    g = golden("s3d_golden.npz")
+    x = torch.from_numpy(s3d_clips(2, 16, 112, seed=int(g["clip_seed"]))).to(DEV)
+    lg, pr = s3d_models[(srm, dt)](x, return_probs=True)
+    torch.cuda.synchronize()
+    p_ref = 1 / (1 + np.exp(-g[f"logits_{srm}"].astype(np.float64)))
+    assert lg.shape == (2, 1)
+    assert np.abs(pr.cpu().numpy() - p_ref).max() <= tol
+
+
+def test_s3d_matches_emulation_tightly(s3d_models, golden):
+    """fp16 path vs the oracle's emulation of its rounding points: logits within 2e-3."""
+    from oracle import s3d_torch as O
+    from fac_fake_amd.weights import make_s3d_state_dict, s3d_clips
+    g = golden("s3d_golden.npz")
+    x = torch.from_numpy(s3d_clips(2, 16, 112, seed=int(g["clip_seed"])))
+    ref = O.forward_emulated(make_s3d_state_dict(0, 1, False), x, False, "fp16")
+    lg = s3d_models[("no", "fp16")](x.to(DEV))
+    torch.cuda.synchronize()
+    assert (lg.cpu() - ref).abs().max() <= 2e-3
+
+
+def test_s3d_graph_replay_matches_eager(s3d_models):
+    from fac_fake_amd.weights import s3d_clips
+    m = s3d_models[("yes", "bf16")]
+    x = torch.from_numpy(s3d_clips(3, 16, 112, seed=5)).to(DEV)
+    eager = m(x).clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        m(x)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            out = m(x)
+    gr.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
