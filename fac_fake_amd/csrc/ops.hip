@@ -72,13 +72,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                    (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
-template <class T, int BM, int BN, int OCC>
-__global__ __launch_bounds__(256, OCC) void convnd_igemm(ConvP p) {
-  constexpr int BK = 64, NS = 3;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+template <class T, int BM, int BN, int WM, int WN, int OCC, int NS>
+__global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
+  constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
+  constexpr int BK = 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int RT = WTM / 16, CT = WTN / 16;
   constexpr int SLOT_A = BM * BK, SLOT = (BM + BN) * BK;  // u16 elements per ring slot
-  constexpr int NA = BM / 32, NB = BN / 32;               // glds per wave per stage (8 rows each)
+  constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW;       // glds per wave per stage (8 rows each)
+  static_assert(NA * 8 * NW == BM && NB * 8 * NW == BN, "tile rows per wave");
   constexpr int PER = NA + NB;
   constexpr int SPITCH = BN + 4;              // fp32 staging row pitch
   constexpr int OPER = NS * SLOT;
@@ -87,25 +89,26 @@ __global__ __launch_bounds__(256, OCC) void convnd_igemm(ConvP p) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   int bx = blockIdx.x;
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);  // XCD-contiguous row tiles
   const int m0 = bx * BM, n0 = blockIdx.y * BN;
 
   // LDS images: rows of 64 k (128 B), the 16-byte piece j of row r at position
   // j ^ ((r >> 1) & 7) (conflict-free ds_read_b128, as in transformer.hip's
-  // gemm_nt).  glds instruction i of this wave fills rows 8*(4i + wave) + lane/8,
+  // gemm_nt).  glds instruction i of this wave fills rows 8*(NW i + wave) + lane/8,
   // position lane % 8, so it copies piece j = (lane % 8) ^ ((row >> 1) & 7) —
   // the same j for all of this lane's instructions, and 8 lanes cover one
   // row's 128 contiguous bytes of K (coalesced when a K step stays in one tap).
   const int pos = lane & 7, rsub = lane >> 3;
+  static_assert(NW % 2 == 0, "4*NW*i must vanish mod 8");
   const int j = pos ^ ((4 * wave + (lane >> 4)) & 7);
   // per A instruction: the output position of its row
   const uint16_t* rbase[NA];
   int riz[NA], riy[NA], rix[NA];
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
-    const int m = m0 + 8 * (4 * i + wave) + rsub;
+    const int m = m0 + 8 * (NW * i + wave) + rsub;
     const int mm = m < p.M ? m : 0;
     const int ox = mm % p.Wo, t1 = mm / p.Wo;
     const int oy = t1 % p.Ho, t2 = t1 / p.Ho;
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256, OCC) void convnd_igemm(ConvP p) {
   trk_norm(t, p.C8, p.KH, p.KW);
   const uint16_t* wsrc[NB];
 #pragma unroll
-  for (int i = 0; i < NB; ++i) wsrc[i] = p.w + (size_t)(n0 + 8 * (4 * i + wave) + rsub) * p.Kp + j * 8;
+  for (int i = 0; i < NB; ++i) wsrc[i] = p.w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * p.Kp + j * 8;
 
   // stage st -> ring slot st % NS; stages past the end copy zeros into slots never read
   auto issue = [&](int st) {
@@ -132,11 +135,11 @@ __global__ __launch_bounds__(256, OCC) void convnd_igemm(ConvP p) {
       const bool ok = real && (unsigned)iz < (unsigned)p.D && (unsigned)iy < (unsigned)p.H &&
                       (unsigned)ix < (unsigned)p.W;
       const uint16_t* src = ok ? rbase[i] + (((size_t)iz * p.H + iy) * p.W + ix) * p.C8 * 8 + t.c8 * 8 : g_zero16;
-      glds16(src, slot + (4 * i + wave) * 64 * 8);
+      glds16(src, slot + (NW * i + wave) * 64 * 8);
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i)
-      glds16(st < p.ksteps ? wsrc[i] + (size_t)st * BK : g_zero16, slot + SLOT_A + (4 * i + wave) * 64 * 8);
+      glds16(st < p.ksteps ? wsrc[i] + (size_t)st * BK : g_zero16, slot + SLOT_A + (NW * i + wave) * 64 * 8);
     t.kp += 8;
     t.c8 += 8;
     trk_norm(t, p.C8, p.KH, p.KW);
@@ -181,12 +184,12 @@ __global__ __launch_bounds__(256, OCC) void convnd_igemm(ConvP p) {
   // vectors.  The residual's 16-byte vectors are loaded first, so their
   // latency overlaps the staging.
   constexpr int QPR = BN / 8;                 // 8-channel pieces per row
-  constexpr int QPT = BM * QPR / 256;         // pieces per thread
+  constexpr int QPT = BM * QPR / NT;          // pieces per thread
   const bool resid = p.flags & FAC_CONV_RESID;
   u16x8 rv[QPT];
 #pragma unroll
   for (int i = 0; i < QPT; ++i) {
-    const int q = tid + i * 256, row = q / QPR, cp = q - row * QPR;
+    const int q = tid + i * NT, row = q / QPR, cp = q - row * QPR;
     const int mo = m0 + row, c = n0 + cp * 8;
     rv[i] = (u16x8)0;
     if (resid && p.vec_res && mo < p.M && c + 8 <= p.Cout)
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(256, OCC) void convnd_igemm(ConvP p) {
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < QPT; ++i) {
-    const int q = tid + i * 256, row = q / QPR, cp = q - row * QPR;
+    const int q = tid + i * NT, row = q / QPR, cp = q - row * QPR;
     const int mo = m0 + row, c = n0 + cp * 8;
     if (mo >= p.M || c >= p.Cout) continue;
     const int nc = min(8, p.Cout - c);
@@ -316,6 +319,44 @@ __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, in
   for (int c = 8; c < c_pad; c += 8) *(u16x8*)(o + c) = (u16x8)0;
 }
 
+// Space-to-depth staging for a stride-2 first conv: image pixel (y, x) goes
+// to s2d pixel (y/2 + pb, x/2 + pb), channel ((y%2)*2 + x%2)*4 + c (c < 3;
+// channel 3 of each pixel and the pb / pa border are zero), so a KxK stride-2
+// conv becomes a stride-1 conv over 2x2-pixel cells with 16 contiguous
+// channels per cell (fac_pack_input_s2d).  One thread per s2d cell.
+template <class T, bool U8>
+__global__ __launch_bounds__(256) void pack_input_s2d(const void* src, int n_img, int frames, int H, int W, int pb,
+                                                      int pa, float div, float m0, float m1, float m2, float s0,
+                                                      float s1, float s2, uint16_t* out) {
+  const int Ho = H / 2 + pb + pa, Wo = W / 2 + pb + pa;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (long long)n_img * Ho * Wo) return;
+  const int X = (int)(t % Wo), Y = (int)((t / Wo) % Ho), n = (int)(t / ((long long)Wo * Ho));
+  const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
+  u16x8 lo = (u16x8)0, hi = (u16x8)0;
+  const int y0 = 2 * (Y - pb), x0 = 2 * (X - pb);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int y = y0 + (d >> 1), x = x0 + (d & 1);
+    if (y < 0 || y >= H || x < 0 || x >= W || Y < pb || X < pb || Y >= Ho - pa || X >= Wo - pa) continue;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float v;
+      if constexpr (U8) {
+        v = (float)((const uint8_t*)src)[(((size_t)n * H + y) * W + x) * 3 + c];
+      } else {  // planar [clip][3][frames][H][W]: image n = clip * frames + frame
+        const int b = n / frames, f = n - b * frames;
+        v = ((const float*)src)[((((size_t)b * 3 + c) * frames + f) * H + y) * W + x];
+      }
+      const uint16_t h = T::from_f32((v / div - mean[c]) / sd[c]);
+      if (d < 2) lo[d * 4 + c] = h; else hi[(d - 2) * 4 + c] = h;
+    }
+  }
+  uint16_t* o = out + (size_t)t * 16;
+  *(u16x8*)o = lo;
+  *(u16x8*)(o + 8) = hi;
+}
+
 // ---- KANLinear
 // Cox-de Boor recursion of kan.py:90-132 for one input value, in the
 // reference's operation order (no contraction: the file is compiled with
@@ -343,6 +384,9 @@ constexpr int kKanRows = 32, kKanIn = 32;
 // grid (in-chunks, row-chunks): features of 32 rows x 32 inputs into LDS,
 // then every (row, out) pair of the chunk accumulates its 32 x 9 products
 // into a partial slab [in-chunk][row][out] (summed in chunk order after).
+// Weights are k-major wcat[in][9][out], so the 64 threads of a row group read
+// 64 consecutive outputs' weights of one k (coalesced) and each feature is an
+// LDS broadcast; a thread keeps 8 rows of one output in registers.
 __global__ __launch_bounds__(256) void kan_partial(const float* __restrict__ x, int rows, int in_f, int out_f,
                                                    const float* __restrict__ grid, const float* __restrict__ wcat,
                                                    float* __restrict__ part) {
@@ -368,12 +412,20 @@ __global__ __launch_bounds__(256) void kan_partial(const float* __restrict__ x, 
   }
   __syncthreads();
   const int K = ni * kKanF;
-  for (int q = threadIdx.x; q < nr * out_f; q += 256) {
-    const int r = q / out_f, o = q - r * out_f;
-    const float* w = wcat + ((size_t)o * in_f + i0) * kKanF;
-    float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc = fmaf(feat[r][k], w[k], acc);
-    part[((size_t)ic * rows + r0 + r) * out_f + o] = acc;
+  const int ol = threadIdx.x & 63, rg = threadIdx.x >> 6;  // 4 row groups of 8 rows
+  const float* w0 = wcat + (size_t)i0 * kKanF * out_f;
+  for (int ob = 0; ob < out_f; ob += 64) {
+    const int o = ob + ol;
+    if (o >= out_f) continue;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < K; ++k) {
+      const float w = w0[(size_t)k * out_f + o];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[r] = fmaf(feat[rg * 8 + r][k], w, acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      if (rg * 8 + r < nr) part[((size_t)ic * rows + r0 + rg * 8 + r) * out_f + o] = acc[r];
   }
 }
 
@@ -392,11 +444,24 @@ __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, fl
 
 template <class T>
 static hipError_t launch_convnd(const ConvP& p, int cout_pad, hipStream_t st) {
-  const int gx = (p.M + 127) / 128;
-  // 128 x 64 tiles, two workgroups per CU (72 KB ring each): measured faster
-  // than 128 x 128 at one per CU on every ResNet-50 layer (tools/rvk_layers.py)
   (void)cout_pad;
-  convnd_igemm<T, 128, 64, 2><<<dim3(gx, (p.Cout + 63) / 64), 256, 0, st>>>(p);
+  const int gx64 = (p.M + 63) / 64, gx128 = (p.M + 127) / 128, gx256 = (p.M + 255) / 256;
+  const int ny64 = (p.Cout + 63) / 64, ny128 = (p.Cout + 127) / 128;
+  if (p.ksteps <= 2) {
+    // K <= 128 (1x1 expansions): memory-bound, so occupancy first — a 2-slot
+    // ring (48 KB) lets three 128 x 64 workgroups share a CU
+    convnd_igemm<T, 128, 64, 2, 2, 3, 2><<<dim3(gx128, ny64), 256, 0, st>>>(p);
+  } else if ((long long)gx128 * ny64 < 512) {
+    // small grids (S3D's late 4x7x7 / 2x3x3 stages): 64 x 64 tiles, three per CU
+    convnd_igemm<T, 64, 64, 2, 2, 3, 3><<<dim3(gx64, ny64), 256, 0, st>>>(p);
+  } else if (p.Cout % 128 == 0 && (long long)gx256 * ny128 >= 448) {
+    // 256 x 128 tiles (8 waves, 144 KB ring, one per CU: 48 KB global -> LDS per
+    // 4.2 MFLOP, twice the 128 x 64 tile's intensity) when the grid still fills
+    // the chip about twice over and no column tile is half empty
+    convnd_igemm<T, 256, 128, 4, 2, 1, 3><<<dim3(gx256, ny128), 512, 0, st>>>(p);
+  } else {
+    convnd_igemm<T, 128, 64, 2, 2, 2, 3><<<dim3(gx128, ny64), 256, 0, st>>>(p);
+  }
   return hipGetLastError();
 }
 
@@ -502,6 +567,32 @@ int fac_pack_input(int dtype, const void* src, int src_kind, int n, int s, float
   uint16_t* o = (uint16_t*)out;
 #define FAC_PACK(TT, U)                                                                                      \
   pack_input<TT, U><<<nb, 256, 0, st>>>(src, n, s, div, m[0], m[1], m[2], sd[0], sd[1], sd[2], o, c_pad)
+  if (dtype == FAC_DTYPE_BF16) {
+    if (src_kind == 0) FAC_PACK(BF16, true); else FAC_PACK(BF16, false);
+  } else {
+    if (src_kind == 0) FAC_PACK(F16, true); else FAC_PACK(F16, false);
+  }
+#undef FAC_PACK
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_pack_input_s2d(int dtype, const void* src, int src_kind, int n, int frames, int h, int w, int pad_before,
+                       int pad_after, float div, const float* mean3, const float* std3, void* out, void* stream) {
+  using namespace fac;
+  if (!src || !out || n <= 0 || frames <= 0 || h <= 0 || w <= 0 || h % 2 || w % 2 || pad_before < 0 || pad_after < 0 ||
+      (src_kind != 0 && src_kind != 1) || !(div > 0.f))
+    return FAC_ERR_ARG;
+  if (dtype != FAC_DTYPE_BF16 && dtype != FAC_DTYPE_F16) return FAC_ERR_ARG;
+  const float m[3] = {mean3 ? mean3[0] : 0.f, mean3 ? mean3[1] : 0.f, mean3 ? mean3[2] : 0.f};
+  const float sd[3] = {std3 ? std3[0] : 1.f, std3 ? std3[1] : 1.f, std3 ? std3[2] : 1.f};
+  const long long total =
+      (long long)n * frames * (h / 2 + pad_before + pad_after) * (w / 2 + pad_before + pad_after);
+  const int nb = (int)((total + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  uint16_t* o = (uint16_t*)out;
+#define FAC_PACK(TT, U)                                                                                         \
+  pack_input_s2d<TT, U><<<nb, 256, 0, st>>>(src, n * frames, frames, h, w, pad_before, pad_after, div, m[0], \
+                                            m[1], m[2], sd[0], sd[1], sd[2], o)
   if (dtype == FAC_DTYPE_BF16) {
     if (src_kind == 0) FAC_PACK(BF16, true); else FAC_PACK(BF16, false);
   } else {

@@ -200,9 +200,54 @@ def pack_input(src: torch.Tensor, *, dtype: str, u8: bool, div: float = 1.0, mea
     return out
 
 
+def pack_input_s2d(src: torch.Tensor, *, dtype: str, u8: bool, div: float = 1.0, mean=None, std=None,
+                   pad_before: int = 2, pad_after: int = 1) -> torch.Tensor:
+    """3-channel images -> 16-bit space-to-depth cells [N, T, h/2+pb+pa, w/2+pb+pa, 16]
+    (fac_pack_input_s2d).  u8: src uint8 [N, h, w, 3] (T = 1); else fp32
+    [N, 3, h, w] (T = 1) or a clip batch [N, 3, T, h, w]."""
+    n = src.shape[0]
+    frames = src.shape[2] if (not u8 and src.dim() == 5) else 1
+    h, w = (src.shape[1], src.shape[2]) if u8 else (src.shape[-2], src.shape[-1])
+    ho, wo = h // 2 + pad_before + pad_after, w // 2 + pad_before + pad_after
+    out = torch.empty(n, frames, ho, wo, 16, device=src.device, dtype=TORCH16[dtype])
+    m = (ctypes.c_float * 3)(*(mean if mean is not None else (0.0, 0.0, 0.0)))
+    sd = (ctypes.c_float * 3)(*(std if std is not None else (1.0, 1.0, 1.0)))
+    src = src.contiguous()
+    _lib.check(_lib.load().fac_pack_input_s2d(_lib.DTYPES[dtype], src.data_ptr(), 0 if u8 else 1, n, frames, h, w,
+                                              pad_before, pad_after, float(div), ctypes.cast(m, ctypes.c_void_p),
+                                              ctypes.cast(sd, ctypes.c_void_p), out.data_ptr(), _stream(src)),
+               None, "fac_pack_input_s2d")
+    return out
+
+
+def s2d_weight(w: torch.Tensor) -> torch.Tensor:
+    """[co, 3, 7, 7] stride-2 pad-3 kernel -> [co, 16, 4, 4] stride-1 kernel over
+    fac_pack_input_s2d cells: w'[o][(dy*2+dx)*4 + c][ty][tx] = w[o][c][2ty+dy-1][2tx+dx-1].
+    A (1, 7, 7) Conv3d kernel maps to (1, 4, 4) the same way."""
+    if w.dim() == 5:
+        if w.shape[2] != 1:
+            raise ValueError("space-to-depth packing is for spatial-only (1, k, k) kernels")
+        return s2d_weight(w[:, :, 0]).unsqueeze(2)
+    co, ci, kh, kw = w.shape
+    if ci != 3 or kh != 7 or kw != 7:
+        raise ValueError("space-to-depth packing is for the 3-channel 7x7/2 first conv")
+    out = torch.zeros(co, 16, 4, 4, dtype=w.dtype)
+    for ty in range(4):
+        for dy in range(2):
+            ky = 2 * ty + dy - 1
+            if not 0 <= ky < 7:
+                continue
+            for tx in range(4):
+                for dx in range(2):
+                    kx = 2 * tx + dx - 1
+                    if 0 <= kx < 7:
+                        out[:, (dy * 2 + dx) * 4:(dy * 2 + dx) * 4 + 3, ty, tx] = w[:, :, ky, kx]
+    return out
+
+
 class KANLinearLayer:
     """KANLinear (CViT-main/ResVitKan/kan.py:18-206) packed for fac_kan_linear:
-    wcat[o][i][0] = base_weight, wcat[o][i][1+k] = spline_weight * spline_scaler."""
+    wcat[i][0][o] = base_weight[o][i], wcat[i][1+k][o] = spline_weight[o][i][k] * spline_scaler[o][i]."""
 
     N_KNOTS = 12
 
@@ -215,7 +260,8 @@ class KANLinearLayer:
         if g.shape != (self.in_f, self.N_KNOTS) or sw.shape != (self.out_f, self.in_f, self.N_KNOTS - 4):
             raise ValueError("KANLinear with grid_size 5 and spline_order 3 expected")
         scaled = sw * ss.unsqueeze(-1)                    # scaled_spline_weight (kan.py:176-183)
-        self.wcat = torch.cat([bw.unsqueeze(-1), scaled], dim=2).contiguous().to(device)
+        # k-major [in][1 + nb][out] (fac_kan_linear)
+        self.wcat = torch.cat([bw.unsqueeze(-1), scaled], dim=2).permute(1, 2, 0).contiguous().to(device)
         self.grid = g.contiguous().to(device)
         self._scratch = None
 

@@ -34,7 +34,7 @@ from torch import nn
 
 from . import _lib
 from .cvit import MAX_SLOTS, _Node
-from .ops import TORCH16, ConvLayer, KANLinearLayer, fold_bn, pack_input, pool, sigmoid
+from .ops import TORCH16, ConvLayer, KANLinearLayer, fold_bn, pack_input_s2d, pool, s2d_weight, sigmoid
 from .weights import kan_grid, resnet50_blocks, resvitkan_param_specs
 
 SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
@@ -133,7 +133,10 @@ class ResVitKan(nn.Module):
                            sd[bnp + ".running_var"], BN_EPS)
             return ConvLayer(w, b, stride, pad, dtype=dt, device=device, cin_pad=cin_pad)
 
-        self._conv1 = conv("features.conv1.weight", "features.bn1", 2, 3, cin_pad=8)
+        # conv1 7x7/2 (3 channels) as a 4x4/1 conv over space-to-depth cells (ops.s2d_weight)
+        w1, b1 = fold_bn(sd["features.conv1.weight"], None, sd["features.bn1.weight"], sd["features.bn1.bias"],
+                         sd["features.bn1.running_mean"], sd["features.bn1.running_var"], BN_EPS)
+        self._conv1 = ConvLayer(s2d_weight(w1), b1, 1, 0, dtype=dt, device=device)
         self._blocks = []
         for p, _inp, _planes, s, ds in resnet50_blocks():
             self._blocks.append((conv(p + ".conv1.weight", p + ".bn1"),
@@ -184,14 +187,15 @@ class ResVitKan(nn.Module):
     feature_chunk = 0
 
     def features16(self, x16: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """ResNet.forward (ResVitKan.py:232-247) on packed 16-bit [B,1,224,224,8]
-        -> [B,1,7,7,512] 16-bit NHWC, in chunks of ``feature_chunk`` crops."""
+        """ResNet.forward (ResVitKan.py:232-247) on space-to-depth packed 16-bit
+        cells [B,1,115,115,16] (ops.pack_input_s2d) -> [B,1,7,7,512] 16-bit
+        NHWC, in chunks of ``feature_chunk`` crops."""
         B = x16.shape[0]
         if out is None:
             out = torch.empty(B, 1, 7, 7, 512, dtype=x16.dtype, device=x16.device)
         step = self.feature_chunk or B
         for b0 in range(0, B, step):
-            x = self._conv1(x16[b0:b0 + step])                      # 7x7/2 + bn1 + ReLU
+            x = self._conv1(x16[b0:b0 + step])                      # 7x7/2 + bn1 + ReLU, on s2d cells
             x = pool(x, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")     # MaxPool2d(3, 2, 1)
             for c1, c2, c3, ds in self._blocks:
                 res = ds(x, relu=False) if ds is not None else x
@@ -221,7 +225,7 @@ class ResVitKan(nn.Module):
         if img.dim() != 4 or tuple(img.shape[1:]) != (3, 224, 224):
             raise ValueError(f"expected img [B,3,224,224], got {tuple(img.shape)}")
         self._prepare(img.device)
-        x16 = pack_input(img.float(), dtype=self.dtype_name, u8=False, spatial=(224, 224))
+        x16 = pack_input_s2d(img.float(), dtype=self.dtype_name, u8=False)
         return self._run(x16, pos_index, False)[0]
 
     def forward_u8(self, crops: torch.Tensor, pos_index=None, return_probs: bool = False):
@@ -231,7 +235,7 @@ class ResVitKan(nn.Module):
         if not crops.is_cuda:
             raise RuntimeError("ResVitKan (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
         self._prepare(crops.device)
-        x16 = pack_input(crops, dtype=self.dtype_name, u8=True, div=255.0, mean=MEAN, std=STD, spatial=(224, 224))
+        x16 = pack_input_s2d(crops, dtype=self.dtype_name, u8=True, div=255.0, mean=MEAN, std=STD)
         logits, probs = self._run(x16, pos_index, return_probs)
         return (logits, probs) if return_probs else logits
 

@@ -28,7 +28,7 @@ from torch import nn
 
 from . import _lib
 from .cvit import _Node
-from .ops import TORCH16, ConvLayer, fold_bn, pack_input, pool, sigmoid
+from .ops import TORCH16, ConvLayer, fold_bn, pack_input, pack_input_s2d, pool, s2d_weight, sigmoid
 from .weights import s3d_base, s3d_param_specs
 
 BN_EPS = 1e-3   # BatchNorm3d(eps=1e-3) in BasicConv3d / SepConv3d (model.py:54,67,71)
@@ -103,6 +103,14 @@ class S3D(nn.Module):
         def sep(p, k, s, pd, cin_pad=None):
             return (bconv(p, (1, s, s), (0, pd, pd), cin_pad, "s"), bconv(p, (s, 1, 1), (pd, 0, 0), None, "t"))
 
+        def sep_s2d(p):
+            # base.0 without SRM: the (1,7,7)/(1,2,2) 3-channel conv as a (1,4,4)/1 conv over
+            # space-to-depth cells of each frame (ops.pack_input_s2d / s2d_weight)
+            w, b = fold_bn(sd[p + ".conv_s.weight"], None, sd[p + ".bn_s.weight"], sd[p + ".bn_s.bias"],
+                           sd[p + ".bn_s.running_mean"], sd[p + ".bn_s.running_var"], BN_EPS)
+            return (ConvLayer(s2d_weight(w), b, 1, 0, dtype=dt, device=device),
+                    bconv(p, (2, 1, 1), (3, 0, 0), None, "t"))
+
         self._srm_conv = None
         if self._srm:
             w = sd["SRM.hpf.weight"]
@@ -110,8 +118,10 @@ class S3D(nn.Module):
         self._layers = []
         for i, L in enumerate(s3d_base(self._srm)):
             p = f"base.{i}"
-            if L[0] == "sep":
-                self._layers.append(("sep", sep(p, L[3], L[4], L[5], cin_pad=32 if (i == 0 and self._srm) else None)))
+            if L[0] == "sep" and i == 0 and not self._srm:
+                self._layers.append(("sep", sep_s2d(p)))
+            elif L[0] == "sep":
+                self._layers.append(("sep", sep(p, L[3], L[4], L[5], cin_pad=32 if i == 0 else None)))
             elif L[0] == "basic":
                 self._layers.append(("basic", bconv(p)))
             elif L[0] == "pool":
@@ -166,7 +176,10 @@ class S3D(nn.Module):
             raise ValueError(f"expected a clip [B,3,T,H,W], got {tuple(x.shape)}")
         self._prepare(x.device)
         B, _, T, H, W = x.shape
-        x16 = pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
+        if self._srm:
+            x16 = pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
+        else:
+            x16 = pack_input_s2d(x.float(), dtype=self.dtype_name, u8=False, pad_before=2, pad_after=1)
         y = self.features16(x16)
         _, t, h, w, _ = y.shape
         y = pool(y, (2, h, w), 1, 0, "avg")                           # F.avg_pool3d(y, (2, H, W), stride=1)

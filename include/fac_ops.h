@@ -98,12 +98,27 @@ int fac_pool_nd(const fac_pool_desc* desc, void* stream);
 int fac_pack_input(int dtype, const void* src, int src_kind, int n, int s, float div, const float* mean3,
                    const float* std3, void* out, int c_pad, void* stream);
 
+/* Space-to-depth staging for a stride-2 first conv (ResNet-50's 7x7/2,
+ * ResVitKan.py:187): [n][h/2 + pad_before + pad_after]^2 cells of 16
+ * channels, cell (Y, X) channel ((dy*2 + dx)*4 + c) = normalised pixel
+ * (2(Y - pad_before) + dy, 2(X - pad_before) + dx), channel c < 3 (zero
+ * outside the image and for c = 3).  A 7x7/2 conv with padding 3 is then a
+ * 4x4/1 conv without padding over this image (pad_before 2, pad_after 1),
+ * with weights w'[o][ty][tx][(dy*2+dx)*4 + c] = w[o][c][2ty+dy-1][2tx+dx-1]:
+ * K = 256 instead of 49 taps x 8 padded channels.  src_kind as in
+ * fac_pack_input; with frames > 1 the fp32 source is a clip batch
+ * [n][3][frames][h][w] (S3D's (1,7,7)/(1,2,2) first conv, model.py:18) and
+ * the output [n][frames][cells][cells][16]. */
+int fac_pack_input_s2d(int dtype, const void* src, int src_kind, int n, int frames, int h, int w, int pad_before,
+                       int pad_after, float div, const float* mean3, const float* std3, void* out, void* stream);
+
 /* KANLinear forward (CViT-main/ResVitKan/kan.py:189-206), fp32:
  *   y = silu(x) · base_weightᵀ + b_splines(x) · (spline_weight ⊙ spline_scaler)ᵀ
  * with order-3 B-spline bases over the per-feature knot vector `grid`
  * [in][n_knots] (kan.py:90-132, the Cox–de Boor recursion in the
- * reference's operation order).  `wcat` is the fused weight [out][in][1 + nb]
- * (column 0 = base_weight, 1.. = scaled spline weights, nb = n_knots - 4).
+ * reference's operation order).  `wcat` is the fused weight, k-major
+ * [in][1 + nb][out] (index 0 = base_weight[o][i], 1.. = the scaled spline
+ * weights spline_weight[o][i][k] * spline_scaler[o][i], nb = n_knots - 4).
  * x [rows][in] fp32 -> y [rows][out] fp32.  `partial` is a scratch buffer of
  * fac_kan_scratch_bytes() bytes. */
 int fac_kan_linear(const float* x, int rows, int in_f, int out_f, const float* grid, int n_knots, const float* wcat,

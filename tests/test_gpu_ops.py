@@ -165,11 +165,11 @@ def test_resvitkan_features_match_emulation(rvk, golden):
     rounding points (fp16): relative error of the [B,7,7,512] features."""
     from oracle import resvitkan_torch as O
     from oracle.cvit_torch import normalize_u8, to_torch_sd
-    from fac_fake_amd.ops import pack_input
+    from fac_fake_amd.ops import pack_input_s2d
     g = golden("resvitkan_golden.npz")
     x = normalize_u8(make_crops(2, seed=int(g["crop_seed"])))
     m = rvk["fp16"]
-    f = m.features16(pack_input(x.to(DEV), dtype="fp16", u8=False, spatial=(224, 224)))
+    f = m.features16(pack_input_s2d(x.to(DEV), dtype="fp16", u8=False))
     torch.cuda.synchronize()
     ref = O.resnet50_emulated(to_torch_sd(make_resvitkan_state_dict(0)), x, "fp16").permute(0, 2, 3, 1)
     err = (f.cpu().float().reshape(ref.shape) - ref).abs().max() / ref.abs().max()

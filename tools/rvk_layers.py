@@ -1,8 +1,9 @@
-"""Per-layer timing of the ResVitKan ResNet-50 stem (fac_conv_nd / fac_pool_nd
-launches) at B crops: each layer's mean event-timed duration over a few eager
-forwards, with its algorithmic TFLOP/s and minimum HBM GB/s.  GPU box only.
+"""Per-layer timing of the fac_conv_nd launches of the ResVitKan ResNet-50 stem
+(--model rvk, B crops) or of S3D (--model s3d, B 16x112x112 clips): each
+layer's median event-timed duration over a few eager forwards, with its
+algorithmic TFLOP/s and minimum HBM GB/s.  GPU box only.
 
-    python tools/rvk_layers.py [--B 256] [--dtype bf16]
+    python tools/rvk_layers.py [--model rvk|s3d] [--B 256] [--dtype bf16]
 """
 import argparse
 import sys
@@ -20,16 +21,28 @@ from fac_fake_amd.weights import make_crops, make_resvitkan_state_dict  # noqa: 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--model", default="rvk", choices=["rvk", "s3d"])
+    ap.add_argument("--B", type=int, default=0)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    m = ResVitKan(dtype=a.dtype)
-    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_resvitkan_state_dict(0).items()})
-    crops = torch.from_numpy(make_crops(a.B, seed=3)).to(dev)
-    pidx = torch.arange(a.B, dtype=torch.int32, device=dev) % 32
-    m.forward_u8(crops, pos_index=pidx)
+    if a.model == "rvk":
+        a.B = a.B or 256
+        m = ResVitKan(dtype=a.dtype)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_resvitkan_state_dict(0).items()})
+        crops = torch.from_numpy(make_crops(a.B, seed=3)).to(dev)
+        pidx = torch.arange(a.B, dtype=torch.int32, device=dev) % 32
+        run = lambda: m.forward_u8(crops, pos_index=pidx)  # noqa: E731
+    else:
+        from fac_fake_amd.s3d import S3D
+        from fac_fake_amd.weights import make_s3d_state_dict, s3d_clips
+        a.B = a.B or 64
+        m = S3D(1, "no", dtype=a.dtype)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, False).items()})
+        clips = torch.from_numpy(s3d_clips(a.B, 16, 112, seed=3)).to(dev)
+        run = lambda: m(clips)  # noqa: E731
+    run()
     torch.cuda.synchronize()
     rec = []
     orig = ops.ConvLayer.__call__
@@ -45,7 +58,8 @@ def main():
         K = self.g.kd * self.g.kh * self.g.kw * self.cin
         flops = 2.0 * M * self.cout * K
         byts = 2.0 * (n * d * h * w * c + M * self.cout * (2 if kw.get("residual") is not None else 1))
-        rec.append((f"{self.g.kh}x{self.g.kw}/{self.g.sh} {self.cin}->{self.cout} @{h}", M, self.cout, K, flops,
+        rec.append((f"{self.g.kd}x{self.g.kh}x{self.g.kw}/{self.g.sd}{self.g.sh} {self.cin}->{self.cout} @{d}x{h}", M,
+                    self.cout, K, flops,
                     byts, e0, e1))
         return out
 
@@ -54,7 +68,7 @@ def main():
     meta = {}
     for _ in range(a.reps):
         rec.clear()
-        m.forward_u8(crops, pos_index=pidx)
+        run()
         torch.cuda.synchronize()
         for i, (name, M, N, K, fl, by, e0, e1) in enumerate(rec):
             acc[i].append(e0.elapsed_time(e1))
