@@ -1,0 +1,4 @@
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rA > gpurun_out/pytest_gpu.log 2>&1 && \
+timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1

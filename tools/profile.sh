@@ -2,7 +2,7 @@
 # GPU-box profiling: rocprofv3 kernel trace + stats, then separate PMC passes
 # for HBM traffic (FETCH_SIZE, WRITE_SIZE; MI355X_MICROARCH.md HBM section).
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/prof
+OUT=$R/gpurun_out/prof${PROF_TAG}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
