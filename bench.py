@@ -207,6 +207,58 @@ def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, w
             "mfma_roofline_fraction": round(v * S3D_FLOP_PER_CLIP / (world * PEAK_TFLOPS[dtype] * 1e12), 4)}
 
 
+REPBN8_FLOP_PER_CROP = 13.2915e9 + 2 * 56 * 56 * 128 * 128 * 9   # CViT + the extra 128->128 conv at 56^2
+
+
+def _graph_throughput(dev, world: int, run, steps: int, warmup: int):
+    """Capture `run` into one hipGraph, replay `warmup` + `steps` times on a
+    side stream; returns (seconds for `steps` replays, max over ranks; output)."""
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        run()
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = run()
+        for _ in range(warmup):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, out
+
+
+def repbn8_measurement(dev, dtype: str, world: int, B: int = 256, steps: int = 10, warmup: int = 3):
+    """the CViT RepBn8 variant (fac_fake_amd/repbn8.py: DEConv
+    folded convs on fac_conv_nd, GGCA, CViT tail with LinearNorm's eps) on B
+    synthetic uint8 crops resident in HBM, slot j mod 32, one hipGraph per
+    step; independent per rank, crops/s summed over ranks."""
+    from fac_fake_amd.repbn8 import CViT as RepBn8
+    from fac_fake_amd.weights import make_repbn8_state_dict
+    m = RepBn8(dtype=dtype)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_repbn8_state_dict(0).items()})
+    m.reserve(B, dev)
+    crops = torch.from_numpy(make_crops(B, seed=60 + int(os.environ.get("RANK", "0")))).to(dev)
+    pidx = (torch.arange(B, device=dev) % 32).to(torch.int32)
+    el, out = _graph_throughput(dev, world, lambda: m.forward_u8(crops, pos_index=pidx), steps, warmup)
+    v = world * B * steps / el
+    assert torch.isfinite(out).all()
+    return {"workload": f"SURVEY 8f-4: CViT RepBn8 variant forward (DEConv, GGCA, LinearNorm), B={B} crops per GPU, "
+                        "hipGraph per step", "value": round(v, 1), "unit": "face-crops/s", "n_gpus": world,
+            "ms_per_step": round(el / steps * 1e3, 3), "dtype": dtype,
+            "mfma_roofline_fraction": round(v * REPBN8_FLOP_PER_CROP / (world * PEAK_TFLOPS[dtype] * 1e12), 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,7 +276,8 @@ def main():
     ap.add_argument("--no-video", action="store_true", help="skip the config-3 video sub-measurement")
     ap.add_argument("--no-resvitkan", action="store_true", help="skip the config-5 ResVitKan sub-measurement")
     ap.add_argument("--no-s3d", action="store_true", help="skip the config-4 S3D sub-measurement")
-    ap.add_argument("--only", choices=["resvitkan", "s3d"], help="run only one sub-measurement (profiling)")
+    ap.add_argument("--no-repbn8", action="store_true", help="skip the RepBn8-variant sub-measurement")
+    ap.add_argument("--only", choices=["resvitkan", "s3d", "repbn8"], help="run only one sub-measurement (profiling)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="fac_set_option knob (include/fac_cvit.h), repeatable")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
@@ -241,6 +294,11 @@ def main():
     if args.only == "resvitkan":
         r = resvitkan_measurement(dev, args.dtype, world, B, steps=args.steps, warmup=args.warmup,
                                   chunk=args.stem_chunk if args.stem_chunk else None)
+        if rank == 0:
+            print(json.dumps(r), flush=True)
+        return
+    if args.only == "repbn8":
+        r = repbn8_measurement(dev, args.dtype, world, B, steps=args.steps, warmup=args.warmup)
         if rank == 0:
             print(json.dumps(r), flush=True)
         return
@@ -417,6 +475,8 @@ def main():
         line["config4"] = s3d_measurement(dev, args.dtype, world)
     if not args.no_resvitkan:
         line["config5"] = resvitkan_measurement(dev, args.dtype, world)
+    if not args.no_repbn8:
+        line["variant_repbn8"] = repbn8_measurement(dev, args.dtype, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(sd, threads)

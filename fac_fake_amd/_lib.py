@@ -69,6 +69,9 @@ SIGNATURES = {
                                       ctypes.c_void_p]),
     "fac_kan_scratch_bytes": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "fac_sigmoid": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "fac_ggca": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_set_stem_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "fac_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     "fac_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),

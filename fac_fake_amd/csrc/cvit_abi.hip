@@ -35,7 +35,7 @@ hipError_t launch_layernorm(int dtype, const float* x, const float* g, const flo
                             hipStream_t st);
 hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipStream_t st);
 hipError_t launch_resid_layernorm(int dtype, float* x, const float* slab, int S, const float* bias, const float* g,
-                                 const float* b, uint16_t* y, int R, hipStream_t st);
+                                 const float* b, uint16_t* y, int R, hipStream_t st, float eps = 1e-5f);
 hipError_t launch_resid_cls(int dtype, const float* x, const float* slab, int S, const float* bias, uint16_t* c, int B,
                             hipStream_t st);
 hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, float scale, hipStream_t st);
@@ -121,6 +121,8 @@ struct fac_ctx {
   bool tail_pending[2] = {false, false};
   int pipe_k = 0;
   int tail_priority = 1;  // option "tail_priority": 1 = high-priority tail stream
+  float ffn_ln_eps = 1e-5f;  // option "ffn_ln_eps_exp" n: eps = 10^-n of the FeedForward PreNorm LayerNorm
+                             // (1e-6 in the RepBn8 variant's LinearNorm, cvit_GGCA_ADD_DEConv_RepBn8.py:48)
   uint16_t* stem_out2 = nullptr;
   int num_cu = 256;
   uint16_t *act0 = nullptr, *act1 = nullptr, *deep0 = nullptr, *deep1 = nullptr, *stem_out = nullptr, *xn = nullptr,
@@ -562,7 +564,7 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
                            c->gemm_var[1]));
     HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
     HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st, c->gemm_var[2]));
-    HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, T.bo, T.ln2_g, T.ln2_b, c->xn, R, st));
+    HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, T.bo, T.ln2_g, T.ln2_b, c->xn, R, st, c->ffn_ln_eps));
     HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st,
                            c->gemm_var[3]));
     HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->hbuf, kMlp, T.w2, kMlp, nullptr, c->slab, kDim, R, kDim, kMlp, SK, st, c->gemm_var[4]));
@@ -652,6 +654,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
       c->gemm_var[i] = value;
       return FAC_OK;
     }
+  if (k == "ffn_ln_eps_exp") {
+    if (value < 1 || value > 12) return set_err(c, FAC_ERR_ARG, "ffn_ln_eps_exp must be 1..12");
+    c->ffn_ln_eps = (float)std::pow(10.0, -value);
+    return FAC_OK;
+  }
   if (k == "tail_priority") {
     if (c->tail_st) return set_err(c, FAC_ERR_ARG, "tail_priority must be set before the first pipelined forward");
     c->tail_priority = value != 0;

@@ -437,6 +437,87 @@ __global__ __launch_bounds__(256) void kan_reduce(const float* __restrict__ part
   y[t] = s;
 }
 
+// GGCA (Global Grouped Coordinate Attention) of the CViT RepBn8 variant,
+// CViT-main/model/cvit_GGCA_ADD_DEConv_RepBn8.py:144-207, fused with the
+// caller's x = x * GGCA(x) (:436-437).  One workgroup per (image, channel
+// group); the group's H x W x CG features go to LDS in fp32, then
+//   h-pools [H][CG] (mean / max over x), w-pools [W][CG] (mean / max over y),
+//   shared_conv: 1x1 CG->CR, BatchNorm(eval, eps 1e-5), ReLU, 1x1 CR->CG on
+//   each of the 2H + 2W pooled vectors,
+//   att_h = sigmoid(z(h_avg) + z(h_max)), att_w likewise,
+//   out = x * ((x * att_h) * att_w)   (the reference's multiplication order)
+// all in fp32, 16-bit output (the patch-embedding GEMM's A operand).
+// Byte work: 49 x 512 x 2 B in and out per crop — negligible next to the convs.
+template <class T>
+__global__ __launch_bounds__(256) void ggca_k(const uint16_t* __restrict__ x, int H, int W, int C, int groups,
+                                              const float* __restrict__ w1, const float* __restrict__ b1,
+                                              const float* __restrict__ bn4, const float* __restrict__ w2,
+                                              const float* __restrict__ b2, uint16_t* __restrict__ out) {
+  constexpr int MAXP = 16 * 16, MAXCG = 256, MAXV = 64, MAXCR = 16;
+  __shared__ float xs[MAXP * MAXCG / 4];      // H*W*CG <= 16384 floats (64 KB)
+  __shared__ float pv[MAXV * MAXCG / 2];      // (2H + 2W) pooled vectors x CG
+  __shared__ float hid[MAXV * MAXCR];
+  const int img = blockIdx.x / groups, gr = blockIdx.x - img * groups;
+  const int CG = C / groups, CR = CG / 16, P = H * W, NV = 2 * H + 2 * W;
+  const int tid = threadIdx.x;
+  const uint16_t* xb = x + (size_t)img * P * C + gr * CG;
+  for (int i = tid; i < P * CG; i += 256) {
+    const int pix = i / CG, c = i - pix * CG;
+    xs[i] = T::to_f32(xb[(size_t)pix * C + c]);
+  }
+  __syncthreads();
+  // pooled vectors: v = 0..H-1 h_avg, H..2H-1 h_max, 2H..2H+W-1 w_avg, 2H+W.. w_max
+  for (int i = tid; i < NV * CG; i += 256) {
+    const int v = i / CG, c = i - v * CG;
+    float acc;
+    if (v < 2 * H) {
+      const int y = v < H ? v : v - H;
+      acc = xs[(y * W) * CG + c];
+      for (int xx = 1; xx < W; ++xx) {
+        const float e = xs[(y * W + xx) * CG + c];
+        acc = v < H ? acc + e : fmaxf(acc, e);
+      }
+      if (v < H) acc = acc / (float)W;
+    } else {
+      const int u = v - 2 * H, xx = u < W ? u : u - W;
+      acc = xs[xx * CG + c];
+      for (int y = 1; y < H; ++y) {
+        const float e = xs[(y * W + xx) * CG + c];
+        acc = u < W ? acc + e : fmaxf(acc, e);
+      }
+      if (u < W) acc = acc / (float)H;
+    }
+    pv[i] = acc;
+  }
+  __syncthreads();
+  for (int i = tid; i < NV * CR; i += 256) {  // 1x1 CG -> CR, BN (eval), ReLU
+    const int v = i / CR, r = i - v * CR;
+    float a = 0.f;
+    for (int c = 0; c < CG; ++c) a += w1[r * CG + c] * pv[v * CG + c];
+    a += b1[r];
+    const float inv = 1.0f / sqrtf(bn4[CR + r] + 1e-5f);
+    a = (a - bn4[r]) * inv * bn4[2 * CR + r] + bn4[3 * CR + r];
+    hid[i] = fmaxf(a, 0.f);
+  }
+  __syncthreads();
+  for (int i = tid; i < NV * CG; i += 256) {  // 1x1 CR -> CG
+    const int v = i / CG, c = i - v * CG;
+    float a = 0.f;
+    for (int r = 0; r < CR; ++r) a += w2[c * CR + r] * hid[v * CR + r];
+    pv[i] = a + b2[c];
+  }
+  __syncthreads();
+  uint16_t* ob = out + (size_t)img * P * C + gr * CG;
+  for (int i = tid; i < P * CG; i += 256) {
+    const int pix = i / CG, c = i - pix * CG;
+    const int y = pix / W, xx = pix - y * W;
+    const float ah = 1.0f / (1.0f + expf(-(pv[y * CG + c] + pv[(H + y) * CG + c])));
+    const float aw = 1.0f / (1.0f + expf(-(pv[(2 * H + xx) * CG + c] + pv[(2 * H + W + xx) * CG + c])));
+    const float v = xs[i];
+    ob[(size_t)pix * C + c] = T::from_f32(v * ((v * ah) * aw));
+  }
+}
+
 __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, float* __restrict__ y, int n) {
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t < n) y[t] = 1.f / (1.f + expf(-x[t]));
@@ -625,6 +706,24 @@ int fac_kan_linear(const float* x, int rows, int in_f, int out_f, const float* g
 int fac_sigmoid(const float* x, float* y, int n, void* stream) {
   if (!x || !y || n <= 0) return FAC_ERR_ARG;
   fac::sigmoid_k<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(x, y, n);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_ggca(int dtype, const void* x, int n, int h, int w, int c, int groups, const float* w1, const float* b1,
+             const float* bn4, const float* w2, const float* b2, void* out, void* stream) {
+  if (!x || !out || !w1 || !b1 || !bn4 || !w2 || !b2 || n <= 0 || h <= 0 || w <= 0 || groups <= 0 || c % groups)
+    return FAC_ERR_ARG;
+  const int cg = c / groups;
+  if (h > 16 || w > 16 || cg % 16 || cg > 256 || h * w * cg > 16384 || (2 * h + 2 * w) * cg > 8192 ||
+      (2 * h + 2 * w) > 64)
+    return FAC_ERR_SHAPE;
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == 0)
+    fac::ggca_k<fac::BF16><<<n * groups, 256, 0, st>>>((const uint16_t*)x, h, w, c, groups, w1, b1, bn4, w2, b2,
+                                                      (uint16_t*)out);
+  else
+    fac::ggca_k<fac::F16><<<n * groups, 256, 0, st>>>((const uint16_t*)x, h, w, c, groups, w1, b1, bn4, w2, b2,
+                                                     (uint16_t*)out);
   return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 

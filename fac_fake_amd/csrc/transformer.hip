@@ -142,11 +142,12 @@ __global__ __launch_bounds__(256, NS <= 3 ? 2 : 1) void gemm_nt(const uint16_t* 
   }
 }
 
-// LayerNorm(1024, eps 1e-5) of one row held by one wave (16 floats per lane:
-// columns i*256 + 4*lane + j) -> 16-bit (PreNorm, cvit.py:13-20).
+// LayerNorm(1024, eps 1e-5 unless given) of one row held by one wave (16 floats
+// per lane: columns i*256 + 4*lane + j) -> 16-bit (PreNorm, cvit.py:13-20).
 template <class T>
 __device__ __forceinline__ void ln_row_store(const f32x4 (&v)[4], const float* __restrict__ g,
-                                             const float* __restrict__ bta, uint16_t* __restrict__ yr, int lane) {
+                                             const float* __restrict__ bta, uint16_t* __restrict__ yr, int lane,
+                                             float eps = 1e-5f) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
@@ -159,7 +160,7 @@ __device__ __forceinline__ void ln_row_store(const f32x4 (&v)[4], const float* _
       const float d = v[i][j] - mean;
       q += d * d;
     }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / 1024.0f) + 1e-5f);
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / 1024.0f) + eps);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = i * 256 + lane * 4;
@@ -236,7 +237,7 @@ template <class T, int S>
 __global__ __launch_bounds__(64) void resid_layernorm(float* __restrict__ x, const float* __restrict__ slab,
                                                       const float* __restrict__ bias, const float* __restrict__ g,
                                                       const float* __restrict__ bta, uint16_t* __restrict__ y,
-                                                      int R) {
+                                                      int R, float eps) {
   const int row = blockIdx.x, lane = threadIdx.x;
   float* xr = x + (size_t)row * 1024;
   f32x4 v[4];
@@ -246,7 +247,7 @@ __global__ __launch_bounds__(64) void resid_layernorm(float* __restrict__ x, con
     v[i] = (slab_sum<S>(slab, R, row, c) + *(const f32x4*)(bias + c)) + *(const f32x4*)(xr + c);
     *(f32x4*)(xr + c) = v[i];
   }
-  ln_row_store<T>(v, g, bta, y + (size_t)row * 1024, lane);
+  ln_row_store<T>(v, g, bta, y + (size_t)row * 1024, lane, eps);
 }
 
 // After the last layer only the CLS rows matter (cvit.py:177): finish their
@@ -466,20 +467,20 @@ hipError_t launch_layernorm(int dtype, const float* x, const float* g, const flo
 
 template <class T>
 static hipError_t resid_ln_t(float* x, const float* slab, int S, const float* bias, const float* g, const float* b,
-                             uint16_t* y, int R, hipStream_t st) {
+                             uint16_t* y, int R, hipStream_t st, float eps) {
   switch (S) {
-    case 1: resid_layernorm<T, 1><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R); break;
-    case 2: resid_layernorm<T, 2><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R); break;
-    case 4: resid_layernorm<T, 4><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R); break;
+    case 1: resid_layernorm<T, 1><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R, eps); break;
+    case 2: resid_layernorm<T, 2><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R, eps); break;
+    case 4: resid_layernorm<T, 4><<<R, 64, 0, st>>>(x, slab, bias, g, b, y, R, eps); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_resid_layernorm(int dtype, float* x, const float* slab, int S, const float* bias, const float* g,
-                                  const float* b, uint16_t* y, int R, hipStream_t st) {
-  if (dtype == 0) return resid_ln_t<BF16>(x, slab, S, bias, g, b, y, R, st);
-  return resid_ln_t<F16>(x, slab, S, bias, g, b, y, R, st);
+                                  const float* b, uint16_t* y, int R, hipStream_t st, float eps) {
+  if (dtype == 0) return resid_ln_t<BF16>(x, slab, S, bias, g, b, y, R, st, eps);
+  return resid_ln_t<F16>(x, slab, S, bias, g, b, y, R, st, eps);
 }
 
 template <class T>

@@ -376,3 +376,103 @@ def s3d_clips(n: int, frames: int, size: int, seed: int) -> np.ndarray:
     values 0..255 (S3D's un-normalised BGR input, S3D-test.py:94-96)."""
     z = splitmix64(np.arange(n * 3 * frames * size * size, dtype=np.uint64), _stream_seed(seed, "clips"))
     return (z >> np.uint64(56)).astype(np.float32).reshape(n, 3, frames, size, size)
+
+
+# ---------------------------------------------------------------- CViT RepBn8
+# CViT-main/model/cvit_GGCA_ADD_DEConv_RepBn8.py::CViT (:343-455): the CViT
+# stem with DEConv blocks (:320-340, five parallel 3x3 / 1-D kernels summed
+# into one 3x3 at eval), GGCA on the 7x7x512 features (:144-207), attention
+# PreNorm = LayerNorm(eps 1e-5), FeedForward PreNorm = LinearNorm, whose eval
+# path is LayerNorm(eps 1e-6) (:22-46).  One entry per conv of features1 /
+# features2 (nn.Sequential indices):
+#   (sequential, index, kind "conv" | "deconv", cin, cout, bn index | None, relu, pool after)
+REPBN8_LAYERS = [
+    ("features1", 0, "conv", 3, 32, 1, True, False),
+    ("features1", 3, "deconv", 32, 32, 4, True, False),
+    ("features1", 6, "deconv", 32, 32, 7, True, True),
+    ("features1", 10, "conv", 32, 64, 11, True, False),
+    ("features1", 13, "deconv", 64, 64, 14, True, False),
+    ("features1", 16, "deconv", 64, 64, 17, True, True),
+    ("features1", 20, "conv", 64, 128, 21, True, False),
+    ("features1", 23, "deconv", 128, 128, 24, True, False),
+    ("features1", 26, "conv", 128, 128, None, False, False),   # :390 Conv2d(128,128) - no BN, no ReLU
+    ("features1", 27, "deconv", 128, 128, None, True, True),   # :391-392 DEConv(128) -> ReLU
+    ("features1", 30, "conv", 128, 256, 31, True, False),
+    ("features1", 33, "deconv", 256, 256, 34, True, False),
+    ("features1", 36, "deconv", 256, 256, 37, True, False),
+    ("features1", 39, "deconv", 256, 256, 40, True, True),
+    ("features2", 0, "conv", 256, 512, 1, True, False),
+    ("features2", 3, "deconv", 512, 512, 4, True, False),
+    ("features2", 6, "deconv", 512, 512, 7, True, False),
+    ("features2", 9, "deconv", 512, 512, 10, True, True),
+]
+DECONV_PARTS = ("conv1_1.conv", "conv1_2.conv", "conv1_3.conv", "conv1_4.conv", "conv1_5")
+
+
+def _deconv_specs(p, c):
+    out = []
+    for part in DECONV_PARTS:
+        shape = (c, c, 3) if part in ("conv1_2.conv", "conv1_3.conv") else (c, c, 3, 3)
+        out += [(f"{p}.{part}.weight", shape, "dconv"), (f"{p}.{part}.bias", (c,), "cbias")]
+    return out
+
+
+def repbn8_param_specs(dim=1024, depth=6, mlp_dim=2048, num_classes=2, channels=512, patch_size=7):
+    """(name, shape, kind) for every key of the RepBn8 CViT's state_dict, in its order."""
+    specs = [("pos_embedding", (32, 1, dim), "emb"), ("cls_token", (1, 1, dim), "emb")]
+    for seq, idx, kind, ci, co, bn, _relu, _pool in REPBN8_LAYERS:
+        p = f"{seq}.{idx}"
+        if kind == "conv":
+            specs += [(f"{p}.weight", (co, ci, 3, 3), "conv"), (f"{p}.bias", (co,), "cbias")]
+        else:
+            specs += _deconv_specs(p, co)
+        if bn is not None:
+            specs += _bn_specs(f"{seq}.{bn}", co)
+    pdim = channels * patch_size ** 2
+    specs += [("patch_to_embedding.weight", (dim, pdim), "lin"), ("patch_to_embedding.bias", (dim,), "lbias")]
+    for l in range(depth):
+        p = f"transformer.layers.{l}"
+        specs += [(f"{p}.0.fn.norm.weight", (dim,), "gamma"), (f"{p}.0.fn.norm.bias", (dim,), "beta"),
+                  (f"{p}.0.fn.fn.to_qkv.weight", (3 * dim, dim), "lin"),
+                  (f"{p}.0.fn.fn.to_out.weight", (dim, dim), "lin"), (f"{p}.0.fn.fn.to_out.bias", (dim,), "lbias"),
+                  (f"{p}.1.fn.norm.warm", (), "warm"), (f"{p}.1.fn.norm.iter", (), "step"),
+                  (f"{p}.1.fn.norm.total_step", (), "step"),
+                  (f"{p}.1.fn.norm.norm1.weight", (dim,), "gamma"), (f"{p}.1.fn.norm.norm1.bias", (dim,), "beta"),
+                  (f"{p}.1.fn.norm.norm2.alpha", (1,), "alpha")]
+        specs += _bn_specs(f"{p}.1.fn.norm.norm2.bn", dim)
+        specs += [(f"{p}.1.fn.fn.net.0.weight", (mlp_dim, dim), "lin"), (f"{p}.1.fn.fn.net.0.bias", (mlp_dim,), "lbias"),
+                  (f"{p}.1.fn.fn.net.2.weight", (dim, mlp_dim), "lin"), (f"{p}.1.fn.fn.net.2.bias", (dim,), "lbias")]
+    specs += [("mlp_head.0.weight", (mlp_dim, dim), "lin"), ("mlp_head.0.bias", (mlp_dim,), "lbias"),
+              ("mlp_head.2.weight", (num_classes, mlp_dim), "head"), ("mlp_head.2.bias", (num_classes,), "lbias")]
+    gc = channels // 4                      # GGCA(512, 7, 7): 4 groups, reduction 16 (:144-172)
+    specs += [("ggca.shared_conv.0.weight", (gc // 16, gc, 1, 1), "conv"), ("ggca.shared_conv.0.bias", (gc // 16,), "cbias")]
+    specs += _bn_specs("ggca.shared_conv.1", gc // 16)
+    specs += [("ggca.shared_conv.3.weight", (gc, gc // 16, 1, 1), "conv"), ("ggca.shared_conv.3.bias", (gc,), "cbias")]
+    specs += _deconv_specs("Deconv", 256)   # self.Deconv = DEConv(256) (:454): in the state_dict, never called
+    return specs
+
+
+def make_repbn8_state_dict(seed: int = 0, **kw) -> "OrderedDict[str, np.ndarray]":
+    """Synthetic RepBn8 weights (same generator).  The five DEConv kernels are
+    drawn at 1/2.8 of the He bound each: their folded sum (with the central-
+    and angular-difference terms) then has about unit gain, so the features
+    stay O(1) through 14 DEConvs (mean |features2| 0.88); LinearNorm's counters are the reference's defaults
+    (warm 0, iter = total_step = 300000) and RepBN (unused at eval) is a
+    plain alpha = 1 / unit BatchNorm."""
+    sd = OrderedDict()
+    for name, shape, kind in repbn8_param_specs(**kw):
+        if kind == "nbt" or kind == "warm":
+            sd[name] = np.array(0, dtype=np.int64)
+        elif kind == "step":
+            sd[name] = np.array(300000, dtype=np.int64)
+        elif kind == "alpha":
+            sd[name] = np.ones(shape, dtype=np.float32)
+        elif kind in ("conv", "dconv"):
+            fan_in = int(np.prod(shape[1:]))
+            a = float(np.sqrt(6.0 / fan_in))
+            if kind == "dconv":
+                a /= 2.8
+            sd[name] = _u(name, shape, seed, -a, a)
+        else:
+            sd[name] = _synthetic(name, shape, kind, seed)
+    return sd

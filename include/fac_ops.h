@@ -125,6 +125,19 @@ int fac_kan_linear(const float* x, int rows, int in_f, int out_f, const float* g
                    float* y, void* partial, void* stream);
 size_t fac_kan_scratch_bytes(int rows, int in_f, int out_f);
 
+/* GGCA(c, h, w, reduction 16, groups) of the CViT RepBn8 variant fused with
+ * its x = x * GGCA(x) — CViT-main/model/cvit_GGCA_ADD_DEConv_RepBn8.py:144-207,
+ * :436-437 — on 16-bit channels-last features x [n][h][w][c]:
+ *   att_h[y][c] = sigmoid(z(mean_x x) + z(max_x x)), att_w likewise over y,
+ *   z = shared_conv: 1x1 (c/groups -> c/groups/16) + BatchNorm(eval, eps
+ *   1e-5) + ReLU + 1x1 back, applied per channel group;
+ *   out = x * ((x * att_h) * att_w), fp32 arithmetic, 16-bit out.
+ * w1 [cr][cg], b1 [cr], bn4 [4][cr] = running_mean, running_var, weight,
+ * bias; w2 [cg][cr], b2 [cg] (fp32; cg = c/groups, cr = cg/16).
+ * h, w <= 16, cg a multiple of 16, h*w*cg <= 16384. */
+int fac_ggca(int dtype, const void* x, int n, int h, int w, int c, int groups, const float* w1, const float* b1,
+             const float* bn4, const float* w2, const float* b2, void* out, void* stream);
+
 /* Row-wise sigmoid of logits (the per-logit pred_sig of the heads). */
 int fac_sigmoid(const float* x, float* y, int n, void* stream);
 

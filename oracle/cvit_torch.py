@@ -62,8 +62,10 @@ def _pos_rows(sd, pos_index, B):
     return pos[torch.as_tensor(pos_index, dtype=torch.long)]
 
 
-def _transformer(sd, x, depth=6, heads=8, lin=None, act_round=None):
-    """6 x {x += to_out(attn(LN(x))); x += FF(LN(x))} (cvit.py:5-78)."""
+def _transformer(sd, x, depth=6, heads=8, lin=None, act_round=None, ff_norm="1.fn.norm", ff_eps=LN_EPS):
+    """6 x {x += to_out(attn(LN(x))); x += FF(LN(x))} (cvit.py:5-78).  ff_norm /
+    ff_eps: the FeedForward PreNorm's LayerNorm (the RepBn8 variant's
+    LinearNorm evaluates LayerNorm(eps 1e-6) at ``1.fn.norm.norm1``)."""
     lin = lin or (lambda inp, w, b=None: F.linear(inp, w, b))
     rnd = act_round or (lambda t: t)
     B, n, dim = x.shape
@@ -76,7 +78,7 @@ def _transformer(sd, x, depth=6, heads=8, lin=None, act_round=None):
         att = (torch.einsum("bhid,bhjd->bhij", q, k) * scale).softmax(dim=-1)
         o = torch.einsum("bhij,bhjd->bhid", att, v).permute(0, 2, 1, 3).reshape(B, n, dim)
         x = lin(rnd(o), sd[p + "0.fn.fn.to_out.weight"], sd[p + "0.fn.fn.to_out.bias"]) + x
-        h = F.layer_norm(x, (dim,), sd[p + "1.fn.norm.weight"], sd[p + "1.fn.norm.bias"], LN_EPS)
+        h = F.layer_norm(x, (dim,), sd[p + ff_norm + ".weight"], sd[p + ff_norm + ".bias"], ff_eps)
         h = F.gelu(lin(rnd(h), sd[p + "1.fn.fn.net.0.weight"], sd[p + "1.fn.fn.net.0.bias"]))
         x = lin(rnd(h), sd[p + "1.fn.fn.net.2.weight"], sd[p + "1.fn.fn.net.2.bias"]) + x
     return x

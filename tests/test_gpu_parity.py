@@ -463,3 +463,4 @@ def test_video_driver_matches_drop_in(models, mode):
     assert len(sel) == (6 if mode == "reference" else 60)
     assert torch.equal(logits.cpu(), ref)
     assert score == float(pre_process_prediction(pred_sig(ref)))
+
