@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
-                                                       int Cin, int Cout, const uint16_t* __restrict__ zero16) {
+                                                       int Cin, int Cout, const uint16_t* __restrict__ zero16,
+                                                       int do_relu) {
   constexpr int CK = CONV_CK;
   constexpr int HH = TH + 2, HWD = TW + 2;
   constexpr int HALO_RP = halo_rp<TW>();
@@ -314,12 +315,12 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       if constexpr (POOL) {
         const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
         const int w = (wm * RTW + rt) * 4 + (lane >> 4);
-        ostg[w * OPS + nl] = T::from_f32(relu(mx + bv));
+        ostg[w * OPS + nl] = T::from_f32(do_relu ? relu(mx + bv) : mx + bv);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int m = (wm * RTW + rt) * 16 + (lane >> 4) * 4 + j;
-          ostg[m * OPS + nl] = T::from_f32(relu(v[j] + bv));
+          ostg[m * OPS + nl] = T::from_f32(do_relu ? relu(v[j] + bv) : v[j] + bv);
         }
       }
     }
@@ -458,37 +459,39 @@ int conv_block_n(int H) {
 
 template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true>
 static void launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
-                       int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st) {
+                       int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if (pool)
     conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
-        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   else
     conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
-        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16);
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
 }
 
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
-                                int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st) {
+                                int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st,
+                                int relu) {
   if (W != H) return hipErrorInvalidValue;
   switch (H) {
-    case 224: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 224: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
     // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
-    case 112: launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
-    case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
-    case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
-    case 14: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st); break;
+    case 112: launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 14: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
-                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st) {
-  if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st);
-  return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st);
+                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st,
+                          bool relu) {
+  if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu);
+  return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu);
 }
 
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,

@@ -22,8 +22,10 @@
 
 namespace fac {
 int conv_block_n(int H);
+void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out);
+void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
-                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st);
+                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, bool relu = true);
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
                         int B, int H, int W, hipStream_t st);
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
@@ -313,21 +315,18 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
       bf[o] = (bconv[o] - mean[o]) * s[o] + bet[o];
     }
     auto wf = [&](int o, int cin, int t) { return w[((size_t)o * ci + cin) * 9 + t] * s[o]; };
+    std::vector<float> wfold((size_t)co * ci * 9);  // BN-folded fp32 [co][ci][9]
+    for (int o = 0; o < co; ++o)
+      for (int cin = 0; cin < ci; ++cin)
+        for (int t = 0; t < 9; ++t) wfold[((size_t)o * ci + cin) * 9 + t] = wf(o, cin, t);
     if (i == 0) {
       std::vector<uint16_t> pk((size_t)32 * 64, 0);
       for (int o = 0; o < 32; ++o)
         for (int t = 0; t < 9; ++t)
           for (int cin = 0; cin < 3; ++cin) pk[(size_t)o * 64 + t * 4 + cin] = to16(c->dtype, wf(o, cin, t));
       if ((rc = upload(c, pk, &c->conv1_w))) return rc;
-      // stem224's K order: k = ((ky*2 + kx/2)*2 + kx%2)*4 + cin (kx = 3 and k >= 48
-      // zero), so one 16-byte lane chunk = two horizontally adjacent taps
-      std::vector<uint16_t> pp((size_t)32 * 64, 0);
-      for (int o = 0; o < 32; ++o)
-        for (int t = 0; t < 9; ++t)
-          for (int cin = 0; cin < 3; ++cin) {
-            const int ky = t / 3, kx = t % 3;
-            pp[(size_t)o * 64 + ((ky * 2 + kx / 2) * 2 + kx % 2) * 4 + cin] = to16(c->dtype, wf(o, cin, t));
-          }
+      std::vector<uint16_t> pp((size_t)32 * 64);
+      fac::pack_stem_conv1(c->dtype, wfold.data(), pp.data());  // stem224's pixel-pair K order (stack_ops.hip)
       if ((rc = upload(c, pp, &c->conv1_wp))) return rc;
       if ((rc = upload(c, bf, &c->conv1_b))) return rc;
     } else {
@@ -336,16 +335,8 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
       L.Cin = ci;
       L.Cout = co;
       L.pool = pool_after(i);
-      const int BN = fac::conv_block_n(H), CK = 32, nch = ci / CK;
       std::vector<uint16_t> pk((size_t)co * ci * 9);
-      size_t q = 0;
-      // [n-block][chunk][tap][q][BN][8]: one tap slice is the LDS image of conv.hip
-      for (int nb = 0; nb < co / BN; ++nb)
-        for (int ch = 0; ch < nch; ++ch)
-          for (int t = 0; t < 9; ++t)
-            for (int qq = 0; qq < CK / 8; ++qq)
-              for (int nl = 0; nl < BN; ++nl)
-                for (int j = 0; j < 8; ++j) pk[q++] = to16(c->dtype, wf(nb * BN + nl, ch * CK + qq * 8 + j, t));
+      fac::pack_conv3x3(c->dtype, H, ci, co, wfold.data(), pk.data());  // the LDS-image order of conv.hip
       if ((rc = upload(c, pk, &L.w))) return rc;
       if ((rc = upload(c, bf, &L.b))) return rc;
     }

@@ -11,13 +11,16 @@ the reference's batch-slot ``pos_embedding`` rule.
 
 Arithmetic (no CPU fallback, every layer is a HIP kernel of libfac_cvit.so):
 
-* The 18 convs of ``features1`` / ``features2``: each DEConv (:320-340) is
-  folded on the host at load time into the single 3x3 kernel its eval
-  forward convolves with (``deconv_fold``, the reference's weight algebra in
-  its op order, fp32), eval BatchNorm is folded on top, and every conv is one
-  ``fac_conv_nd`` launch (16-bit NHWC activations, fp32 accumulation, ReLU in
-  the epilogue where the reference has one — not after ``features1.26``,
-  :390-392); ``MaxPool2d(2,2)`` is ``fac_pool_nd``.
+* The 18 convs of ``features1`` / ``features2`` run on the CViT's own
+  conv-stack kernels: each DEConv (:320-340) is folded on the host at load
+  time into the single 3x3 kernel its eval forward convolves with
+  (``deconv_fold``, the reference's weight algebra in its op order, fp32),
+  eval BatchNorm is folded on top; the first block (conv, DEConv, DEConv,
+  pool — the CViT's conv1-3 shape) is the fused ``fac_stem224`` kernel with
+  the input normalisation, every later conv one ``fac_conv3x3`` launch
+  (halo-staged implicit GEMM, 16-bit NHWC, fp32 accumulation, the 2x2
+  max-pool and the ReLU in its epilogue — no ReLU after ``features1.26``,
+  :390-392).
 * ``x = x * GGCA(x)`` (:144-207, :436-437) is one ``fac_ggca`` launch.
 * Patch embedding, cls/pos, the transformer and the head are the CViT tail
   kernels (``fac_forward_features`` on a "tail_only" context); the
@@ -36,15 +39,13 @@ from torch import nn
 
 from . import _lib
 from .cvit import MAX_SLOTS, _Node
-from .ops import TORCH16, ConvLayer, fold_bn, pack_input, pool, sigmoid
+from .ops import TORCH16, fold_bn, sigmoid
 from .weights import REPBN8_LAYERS, repbn8_param_specs
 
 SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
                  mlp_dim=2048)
 BN_EPS = 1e-5
 FF_LN_EPS_EXP = 6                 # LinearNorm.norm1 = LayerNorm(eps=1e-6) (:48)
-MEAN = (0.485, 0.456, 0.406)      # cvit_prediction.py:41-42
-STD = (0.229, 0.224, 0.225)
 _BUFFERS = ("rmean", "rvar", "nbt", "warm", "step")
 
 
@@ -175,8 +176,33 @@ class CViT(nn.Module):
             return
         sd = self.state_dict()
         dt = self.dtype_name
-        self._convs = [(ConvLayer(w, b, 1, 1, dtype=dt, device=device, cin_pad=8 if i == 0 else None), relu, pl)
-                       for i, (w, b, relu, pl) in enumerate(self.folded_layers())]
+        lib = _lib.load()
+        dti = _lib.DTYPES[dt]
+
+        def packed(w, H):
+            co, ci = w.shape[:2]
+            wf = w.reshape(co, ci, 9).contiguous()
+            if H == 0:   # the fused block's conv 3->32
+                out = torch.empty(32 * 64, dtype=torch.int16)
+                _lib.check(lib.fac_stem224_pack_conv1(dti, wf.data_ptr(), out.data_ptr()), None, "pack_conv1")
+            else:
+                n = lib.fac_conv3x3_packed_elems(H, ci, co)
+                if n == 0:
+                    raise ValueError(f"conv {ci}->{co} at {H}x{H} is not a fac_conv3x3 shape")
+                out = torch.empty(n, dtype=torch.int16)
+                _lib.check(lib.fac_conv3x3_pack(dti, H, ci, co, wf.data_ptr(), out.data_ptr()), None, "pack_conv3x3")
+            return out.view(TORCH16[dt]).to(device)
+
+        layers, H = [], 224
+        for i, (w, b, relu, pl) in enumerate(self.folded_layers()):
+            co, ci = w.shape[:2]
+            layers.append((packed(w, 0 if i == 0 else H), b.to(device), H, ci, co, pl, relu))
+            if pl:
+                H //= 2
+        (w1, b1, *_), (w2, b2, *_), (w3, b3, *_) = layers[:3]
+        self._stem = (w1, b1, w2, b2, w3, b3)
+        self._layers = layers[3:]
+        self._zero = torch.zeros(128, dtype=torch.int16, device=device)   # zero-padding source page
         g = "ggca.shared_conv."
         f32 = lambda t: t.detach().to(device=device, dtype=torch.float32).contiguous()  # noqa: E731
         cr, cg = sd[g + "0.weight"].shape[:2]
@@ -186,7 +212,6 @@ class CViT(nn.Module):
                       f32(sd[g + "3.weight"].reshape(cg, cr)), f32(sd[g + "3.bias"]))
         # the CViT tail (embedding .. head) on a context without a conv stem; the
         # FeedForward PreNorm's LayerNorm is LinearNorm.norm1 (eval branch, :40-41)
-        lib = _lib.load()
         self._release()
         h = ctypes.c_void_p()
         _lib.check(lib.fac_create(idx, _lib.DTYPES[dt], ctypes.byref(h)), None, "fac_create")
@@ -222,19 +247,29 @@ class CViT(nn.Module):
         _lib.check(_lib.load().fac_reserve(self._ctx, int(max_batch)), self._ctx, "fac_reserve")
 
     # ------------------------------------------------------------------ forward
-    def features16(self, x16: torch.Tensor) -> torch.Tensor:
-        """features1 + features2 (:432-435) on packed 16-bit [B,1,224,224,8] ->
-        [B,1,7,7,512] 16-bit NHWC."""
-        x = x16
-        for conv, relu, pl in self._convs:
-            x = conv(x, relu=relu)
-            if pl:
-                x = pool(x, (1, 2, 2), (1, 2, 2), 0, "max")
+    def features(self, src: torch.Tensor, u8: bool) -> torch.Tensor:
+        """features1 + features2 (:432-435) -> [B,7,7,512] 16-bit NHWC.  src:
+        uint8 NHWC crops (u8) or normalised fp32 NCHW images."""
+        lib = _lib.load()
+        dti = _lib.DTYPES[self.dtype_name]
+        B, dev = src.shape[0], src.device
+        st = torch.cuda.current_stream(dev).cuda_stream
+        x = torch.empty(B, 112, 112, 32, dtype=TORCH16[self.dtype_name], device=dev)
+        w1, b1, w2, b2, w3, b3 = self._stem
+        _lib.check(lib.fac_stem224(dti, int(u8), src.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                                   b2.data_ptr(), w3.data_ptr(), b3.data_ptr(), x.data_ptr(), B, st), None,
+                   "fac_stem224")
+        for wpk, b, H, ci, co, pl, relu in self._layers:
+            Ho = H // 2 if pl else H
+            y = torch.empty(B, Ho, Ho, co, dtype=x.dtype, device=dev)
+            _lib.check(lib.fac_conv3x3(dti, x.data_ptr(), wpk.data_ptr(), b.data_ptr(), y.data_ptr(), B, H, ci, co,
+                                       int(pl), int(relu), self._zero.data_ptr(), st), None, "fac_conv3x3")
+            x = y
         return x
 
     def weighted_features16(self, f: torch.Tensor) -> torch.Tensor:
-        """x * GGCA(x) (:436-437) on [B,1,7,7,512] 16-bit NHWC."""
-        B, _d, H, W, C = f.shape
+        """x * GGCA(x) (:436-437) on [B,(1,)7,7,512] 16-bit NHWC."""
+        B, (H, W, C) = f.shape[0], f.shape[-3:]
         out = torch.empty_like(f)
         w1, b1, bn4, w2, b2 = self._ggca
         _lib.check(_lib.load().fac_ggca(_lib.DTYPES[self.dtype_name], f.data_ptr(), B, H, W, C, 4, w1.data_ptr(),
@@ -242,11 +277,11 @@ class CViT(nn.Module):
                                         torch.cuda.current_stream(f.device).cuda_stream), None, "fac_ggca")
         return out
 
-    def _run(self, x16: torch.Tensor, pos_index, want_probs: bool):
-        B = x16.shape[0]
-        dev = x16.device
+    def _run(self, src: torch.Tensor, u8: bool, pos_index, want_probs: bool):
+        B = src.shape[0]
+        dev = src.device
         pidx = _pos_index(B, pos_index, dev)
-        f = self.weighted_features16(self.features16(x16))
+        f = self.weighted_features16(self.features(src, u8))
         logits = torch.empty(B, SUPPORTED["num_classes"], dtype=torch.float32, device=dev)
         probs = torch.empty_like(logits) if want_probs else None
         _lib.check(_lib.load().fac_forward_features(self._ctx, f.data_ptr(), B, pidx.data_ptr(), None,
@@ -264,19 +299,17 @@ class CViT(nn.Module):
         if img.dim() != 4 or tuple(img.shape[1:]) != (3, 224, 224):
             raise ValueError(f"expected img [B,3,224,224], got {tuple(img.shape)}")
         self._prepare(img.device)
-        x16 = pack_input(img.float(), dtype=self.dtype_name, u8=False, spatial=(224, 224))
-        return self._run(x16, pos_index, False)[0]
+        return self._run(img.float().contiguous(), False, pos_index, False)[0]
 
     def forward_u8(self, crops: torch.Tensor, pos_index=None, return_probs: bool = False):
-        """uint8 NHWC RGB crops [B,224,224,3]; x/255 + Normalize fused into the input packing."""
+        """uint8 NHWC RGB crops [B,224,224,3]; x/255 + Normalize fused into the first conv block."""
         if crops.dtype != torch.uint8 or crops.dim() != 4 or tuple(crops.shape[1:]) != (224, 224, 3):
             raise ValueError(f"expected uint8 crops [B,224,224,3], got {crops.dtype} {tuple(crops.shape)}")
         if not crops.is_cuda:
             raise RuntimeError("CViT RepBn8 (gfx950 HIP path) needs its input on a GPU device; there is no CPU "
                                "fallback")
         self._prepare(crops.device)
-        x16 = pack_input(crops, dtype=self.dtype_name, u8=True, div=255.0, mean=MEAN, std=STD, spatial=(224, 224))
-        logits, probs = self._run(x16, pos_index, return_probs)
+        logits, probs = self._run(crops.contiguous(), True, pos_index, return_probs)
         return (logits, probs) if return_probs else logits
 
 

@@ -138,6 +138,36 @@ size_t fac_kan_scratch_bytes(int rows, int in_f, int out_f);
 int fac_ggca(int dtype, const void* x, int n, int h, int w, int c, int groups, const float* w1, const float* b1,
              const float* bn4, const float* w2, const float* b2, void* out, void* stream);
 
+/* The CViT conv-stack kernels as layers (fac_cvit.h runs them inside its
+ * fused forward; the CViT variants of the reference stack them differently —
+ * the RepBn8 variant, SURVEY §8f-4, whose DEConv blocks fold into plain 3x3
+ * convs, fac_fake_amd/repbn8.py).  Activations 16-bit NHWC.
+ *
+ * fac_conv3x3: Conv2d(3x3, stride 1, padding 1) + folded BN (+ ReLU if relu)
+ * (+ MaxPool2d(2,2) if pool) — cvit.py:86-148 — on the halo-staged implicit
+ * GEMM of conv.hip: in [n][h][h][cin] -> out [n][h'][h'][cout] (h' = h/2 with
+ * pool); h in {112, 56, 28, 14} (224: cout 32, the unfused kernel), cin a
+ * multiple of 32, cout a multiple of the resolution's block (64 at 112, 128
+ * at 56 and 14, 256 at 28).  wpk: fac_conv3x3_pack of the folded fp32 weight
+ * [cout][cin][3][3]; bias fp32 [cout]; zero256: 256 zero bytes of device
+ * memory (the source of zero-padding loads).
+ * fac_conv3x3_packed_elems: 16-bit elements of the packed weight (0: shape
+ * not supported).  Packing runs on the host (host pointers). */
+size_t fac_conv3x3_packed_elems(int h, int cin, int cout);
+int fac_conv3x3_pack(int dtype, int h, int cin, int cout, const float* w, uint16_t* out);
+int fac_conv3x3(int dtype, const void* in, const void* wpk, const float* bias, void* out, int n, int h, int cin,
+                int cout, int pool, int relu, const void* zero256, void* stream);
+
+/* The fused 224x224 block (stem224.hip): input normalisation, conv 3->32,
+ * conv 32->32, conv 32->32 (each + folded BN + ReLU), MaxPool2d(2,2) ->
+ * [n][112][112][32].  u8: uint8 NHWC crops [n][224][224][3] (x/255 and
+ * Normalize fused); else normalised fp32 NCHW [n][3][224][224].  w1p:
+ * fac_stem224_pack_conv1 of the folded [32][3][3][3] conv-1 weight (host ->
+ * host, 32 x 64 16-bit); w2, w3: fac_conv3x3_pack with h = 224. */
+int fac_stem224_pack_conv1(int dtype, const float* w, uint16_t* out);
+int fac_stem224(int dtype, int u8, const void* in, const void* w1p, const float* b1, const void* w2, const float* b2,
+                const void* w3, const float* b3, void* out, int n, void* stream);
+
 /* Row-wise sigmoid of logits (the per-logit pred_sig of the heads). */
 int fac_sigmoid(const float* x, float* y, int n, void* stream);
 

@@ -146,10 +146,7 @@ def test_repbn8_features_match_emulation(rb8, torch_threads):
     m = rb8["fp16"]
     with torch.no_grad():
         m.forward_u8(torch.from_numpy(crops).to(DEV))   # prepares the packed layers
-        from fac_fake_amd.ops import pack_input
-        xp = pack_input(torch.from_numpy(crops).to(DEV), dtype="fp16", u8=True, div=255.0,
-                        mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), spatial=(224, 224))
-        f = m.features16(xp)[:, 0].float().cpu()
+        f = m.features(torch.from_numpy(crops).to(DEV), u8=True).float().cpu()
     _, ref, _ = O.forward_emulated(make_repbn8_state_dict(0), normalize_u8(crops), dtype="fp16", return_features=True)
     ref = ref.permute(0, 2, 3, 1)
     rel = float((f - ref).norm() / ref.norm())
