@@ -48,7 +48,7 @@ hipError_t launch_crop_resize(const uint8_t* frames, int n_frames, int H, int W,
                               uint8_t* crops, hipStream_t st);
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
-                          hipStream_t st);
+                          hipStream_t s, int* sched = nullptr);
 enum { EPI_F32 = 0, EPI_F32_RELU = 1, EPI_T_GELU = 2, EPI_RESID = 3, EPI_PARTIAL = 4, EPI_T = 5 };
 }  // namespace fac
 
@@ -132,6 +132,8 @@ struct fac_ctx {
   int cap_chunk = 0;  // crops act0/act1 hold
   float *slab = nullptr, *x = nullptr, *qkv = nullptr, *hh = nullptr;
   int* errflag = nullptr;
+  int* sched = nullptr;  // 2 ints: stem224 dynamic box counter + finished-workgroup count
+  int stem_dynamic = 1;  // option "stem_dynamic": stem224 claims boxes from `sched` (else static)
   uint16_t* zero16 = nullptr;  // 256 zero bytes: the source of zero-padding glds pieces
 };
 
@@ -163,7 +165,7 @@ hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, ui
 }
 
 struct WsLayout {
-  size_t act, deep, stem, stem2, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
+  size_t act, deep, stem, stem2, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, sched, zero, total;
   int cb;  // crops the high-res activation buffers hold (stem chunk)
 };
 
@@ -194,6 +196,7 @@ WsLayout layout(int B, int chunk) {
   L.cbuf = off; off += al((size_t)B * kDim * 2);
   L.hh = off; off += al((size_t)B * kMlp * 4);
   L.err = off; off += 256;
+  L.sched = off; off += 256;
   L.zero = off; off += 256;
   L.total = off;
   return L;
@@ -231,6 +234,7 @@ int ensure_ws(fac_ctx* c, int B) {
   c->cbuf = (uint16_t*)(base + L.cbuf);
   c->hh = (float*)(base + L.hh);
   c->errflag = (int*)(base + L.err);
+  c->sched = (int*)(base + L.sched);  // stem224 box counters (zeroed above, self-resetting)
   c->zero16 = (uint16_t*)(base + L.zero);  // the whole workspace was just zeroed
   c->ws_bytes = L.total;
   c->cap_B = B;
@@ -461,7 +465,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     if (c->fuse_stem224 && (stop_after < 0 || stop_after >= 2)) {
       // conv1..conv3 + pool in one kernel; the profile reports it as stage 0 (conv1)
       HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_wp, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
-                                c->conv[1].b, cur, nb, c->num_cu, st));
+                                c->conv[1].b, cur, nb, c->num_cu, st, c->stem_dynamic ? c->sched : nullptr));
       MARK(0);
       l0 = 2;
       if (stop_after == 2) {
@@ -636,6 +640,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   }
   if (k == "fuse_stem224") {
     c->fuse_stem224 = value != 0;
+    return FAC_OK;
+  }
+  if (k == "stem_dynamic") {
+    c->stem_dynamic = value != 0;
     return FAC_OK;
   }
   static const char* gemm_keys[6] = {"gemm_patch", "gemm_qkv", "gemm_out", "gemm_ff1", "gemm_ff2", "gemm_head"};

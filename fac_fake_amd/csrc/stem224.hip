@@ -38,6 +38,53 @@ __device__ __forceinline__ void win_pixel(int m, int& py, int& px) {
   px = 2 * wx + (sub & 1);
 }
 
+// The nine taps of one 3x3 conv stage over NT row tiles per wave,
+// software-pipelined: tap t multiplies fragments read during tap t-1, and
+// right behind each row tile's two MFMAs that tile's fragment for tap t+1 is
+// read (the weights of tap t+1 ahead of the first tile).  The reads then
+// overlap the MFMAs instead of each MFMA pair waiting on the read issued just
+// before it (the compiler's own order: one read in flight per wave).
+// TR: transposed orientation (C^T = W . X^T, conv2) or normal (conv3).
+// img + rd[i]: tile i's fragment for tap 0; tap (ky,kx) is ky*RP + kx pixel
+// slots further.  wl: this lane's weight row; tap t, channel tile ct at
+// wl + (t*128 + ct*16)*8 (weights [tap][q][32][8]).
+template <class T, bool TR, int NT, int RP>
+__device__ __forceinline__ void tap_pipeline(f32x4 (&acc)[NT][2], const uint16_t* img, const int (&rd)[NT],
+                                             const uint16_t* wl) {
+  u16x8 fa[NT], wf[2];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) fa[i] = *(const u16x8*)(img + rd[i]);
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(wl + ct * 16 * 8);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ntoff = (((t + 1) / 3) * RP + (t + 1) % 3) * 8;
+    u16x8 wn[2];
+    if (t < 8) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) wn[ct] = *(const u16x8*)(wl + ((t + 1) * 128 + ct * 16) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+        acc[i][ct] = TR ? T::mfma(wf[ct], fa[i], acc[i][ct]) : T::mfma(fa[i], wf[ct], acc[i][ct]);
+      if (t < 8) fa[i] = *(const u16x8*)(img + rd[i] + ntoff);
+    }
+    if (t < 8) {
+      wf[0] = wn[0];
+      wf[1] = wn[1];
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 constexpr float kNormMean[3] = {0.485f, 0.456f, 0.406f};  // cvit_prediction.py:41
 constexpr float kNormStd[3] = {0.229f, 0.224f, 0.225f};   // cvit_prediction.py:42
 
@@ -49,7 +96,8 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
                                                         const float* __restrict__ b2,
                                                         const uint16_t* __restrict__ w3g,
                                                         const float* __restrict__ b3,
-                                                        uint16_t* __restrict__ out, int ntiles) {
+                                                        uint16_t* __restrict__ out, int ntiles,
+                                                        int* __restrict__ sched) {
   constexpr int IMG = 224, TPR = 7, TPI = 98;     // 16x32 boxes per box row / per image
   constexpr int BW = 32;                          // box width (height 16)
   constexpr int IW = BW + 6, IN_PIX = 22 * IW;    // input region 22 x 38
@@ -171,9 +219,25 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       }
     }
   };
-  fetch(blockIdx.x);
+  // Box schedule.  sched == nullptr: static, box blockIdx.x + k*gridDim.x.
+  // Otherwise dynamic: boxes are claimed from the counter sched[0] one box
+  // ahead (the claim for box j+1 is made at the start of box j, so its pixels
+  // can be prefetched during box j), and a workgroup that starts late -- its
+  // CU still held by another stream's kernel -- simply claims fewer boxes
+  // instead of finishing its fixed share last.  s_tile[(j+1)&1] holds the
+  // claim for box j+1; every reader of a slot is past two barriers before
+  // thread 0 overwrites it.  The last workgroup out resets the counters.
+  __shared__ int s_tile[2];
+  int tile = blockIdx.x;
+  if (sched) {
+    if (tid == 0) s_tile[0] = atomicAdd(sched, 1);
+    __syncthreads();
+    tile = s_tile[0];
+  }
+  fetch(tile);
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int j = 0; tile < ntiles; ++j) {
+    if (sched && tid == 0) s_tile[(j + 1) & 1] = atomicAdd(sched, 1);
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
     const int y0 = ty * 16, x0 = tx * BW;
@@ -209,6 +273,11 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     const bool interior = ty > 0 && ty < IMG / 16 - 1 && tx > 0 && tx < TPR - 1;
 
     // ---- B: conv1 over the 20x36 region at (y0-2, x0-2): 45 row tiles, raster order
+    u16x8 w1f[2][2];  // this lane's conv1 weight fragments [ks][ct], read once per box
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) w1f[ks][ct] = *(const u16x8*)(sw1 + (ct * 16 + r16) * W1P + ks * 32 + g * 8);
 #pragma unroll
     for (int i = 0; i < N1; ++i) {
       const int rt = wave + 8 * i;
@@ -218,10 +287,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       for (int ks = 0; ks < 2; ++ks) {
         const u16x8 p = *(const u16x8*)(sin + in_off[i][ks]);
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) {
-          const u16x8 wf = *(const u16x8*)(sw1 + (ct * 16 + r16) * W1P + ks * 32 + g * 8);
-          acc[ct] = T::mfma(wf, p, acc[ct]);
-        }
+        for (int ct = 0; ct < 2; ++ct) acc[ct] = T::mfma(w1f[ks][ct], p, acc[ct]);
       }
       bool inside = true;
       if (!interior) {
@@ -241,9 +307,13 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     }
     __syncthreads();
 
-    fetch(tile + gridDim.x);  // next box's pixels land while conv2/conv3 run
+    const int next = sched ? s_tile[(j + 1) & 1] : tile + gridDim.x;
+    fetch(next);  // next box's pixels land while conv2/conv3 run
 
     // ---- C: conv2 over the 18x34 region at (y0-1, x0-1): window-major, 39 row tiles
+    // (wave 7's fifth tile is a dummy over pixel 0, computed and not stored:
+    // waves 0-6 own five tiles, so it costs no time and keeps the tap steps
+    // branch-free for the software pipeline below)
     {
       f32x4 acc[N2][2];
 #pragma unroll
@@ -251,24 +321,9 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         acc[i][0] = bt2[0];
         acc[i][1] = bt2[1];
       }
-      const bool hasN = wave + 8 * (N2 - 1) < RT2;  // waves 0-6 own five row tiles, wave 7 four
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int toff = ((t / 3) * RP + (t % 3)) * 8;
-        u16x8 wf[2];
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw2 + ((t * 4 + g) * 32 + ct * 16 + r16) * 8);
-#pragma unroll
-        for (int i = 0; i < N2; ++i) {
-          if (i == N2 - 1 && !hasN) continue;
-          const u16x8 a = *(const u16x8*)(c1 + c2_rd[i] + toff);
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(wf[ct], a, acc[i][ct]);
-        }
-      }
+      tap_pipeline<T, true, N2, RP>(acc, c1, c2_rd, sw2 + (g * 32 + r16) * 8);
 #pragma unroll
       for (int i = 0; i < N2; ++i) {
-        if (i == N2 - 1 && !hasN) continue;
         const int m = (wave + 8 * i) * 16 + r16;
         bool keep = m < C2_PIX;
         if (!interior && keep) {
@@ -297,19 +352,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         acc[i][0] = bn3[0];
         acc[i][1] = bn3[1];
       }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int toff = ((t / 3) * RP + (t % 3)) * 8;
-        u16x8 wf[2];
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw3 + ((t * 4 + g) * 32 + ct * 16 + r16) * 8);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const u16x8 a = *(const u16x8*)(c2 + c3_rd[i] + toff);
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(a, wf[ct], acc[i][ct]);
-        }
-      }
+      tap_pipeline<T, false, 4, RP>(acc, c2, c3_rd, sw3 + (g * 32 + r16) * 8);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -326,20 +369,27 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       *(u16x8*)(out + (((size_t)b * 112 + (y0 >> 1) + wy) * 112 + (x0 >> 1) + wx) * 32 + q * 8) =
           *(const u16x8*)(ostg + w * 40 + q * 8);
     }
+    tile = next;
+  }
+  // every claim of every workgroup precedes its arrival here: the last one
+  // to arrive leaves both counters at zero for the next launch
+  if (sched && tid == 0 && atomicAdd(sched + 1, 1) == (int)gridDim.x - 1) {
+    atomicExch(sched, 0);
+    atomicExch(sched + 1, 0);
   }
 }
 
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
-                          hipStream_t st) {
+                          hipStream_t st, int* sched) {
   const int ntiles = B * 98;  // 16x32 boxes
   const int grid = nwg < ntiles ? nwg : ntiles;
   if (dtype == 0) {
-    if (u8) stem224_fused<BF16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
-    else stem224_fused<BF16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
+    if (u8) stem224_fused<BF16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
+    else stem224_fused<BF16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
   } else {
-    if (u8) stem224_fused<F16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
-    else stem224_fused<F16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles);
+    if (u8) stem224_fused<F16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
+    else stem224_fused<F16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
   }
   return hipGetLastError();
 }

@@ -164,7 +164,9 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * "gemm_patch" / "gemm_qkv" / "gemm_out" / "gemm_ff1" / "gemm_ff2" /
  * "gemm_head" (GEMM tile variant -1..3 per call site), "proj_splits" (split-K
  * of to_out and FF2: 1, 2 or 4), "tail_only" (before fac_load_weights: no
- * conv stem, fac_forward_features only), "tail_priority", "ffn_ln_eps_exp" (n:
+ * conv stem, fac_forward_features only), "tail_priority", "stem_dynamic" (1 =
+ * the fused stem claims boxes from a device counter, the default; 0 = static
+ * box schedule), "ffn_ln_eps_exp" (n:
  * the FeedForward PreNorm LayerNorm uses eps = 10^-n; default 5, the RepBn8
  * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48). */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
