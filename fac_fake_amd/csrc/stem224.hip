@@ -88,6 +88,23 @@ __device__ __forceinline__ void tap_pipeline(f32x4 (&acc)[NT][2], const uint16_t
 constexpr float kNormMean[3] = {0.485f, 0.456f, 0.406f};  // cvit_prediction.py:41
 constexpr float kNormStd[3] = {0.229f, 0.224f, 0.225f};   // cvit_prediction.py:42
 
+// Phase stamps (wave 0, per box, after each barrier) for tools/ubench/stem_ubench.hip only.
+#ifdef STEM_STAMPS
+__device__ unsigned long long stem_st[4][32][5];
+#define STEM_STAMP(k)                                                                          \
+  do {                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    unsigned long long t_;                                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    if (blockIdx.x < 4 && tid == 0 && j < 32) stem_st[blockIdx.x][j][(k)] = t_;               \
+  } while (0)
+#else
+#define STEM_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 template <class T, bool U8>
 __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__ in_,
                                                         const uint16_t* __restrict__ w1g,
@@ -221,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   };
   // Box schedule.  sched == nullptr: static, box blockIdx.x + k*gridDim.x.
   // Otherwise dynamic: boxes are claimed from the counter sched[0] one box
-  // ahead (the claim for box j+1 is made at the start of box j, so its pixels
+  // ahead (the claim for box j+1 is made during box j, so its pixels
   // can be prefetched during box j), and a workgroup that starts late -- its
   // CU still held by another stream's kernel -- simply claims fewer boxes
   // instead of finishing its fixed share last.  s_tile[(j+1)&1] holds the
@@ -237,11 +254,15 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   fetch(tile);
 
   for (int j = 0; tile < ntiles; ++j) {
-    if (sched && tid == 0) s_tile[(j + 1) & 1] = atomicAdd(sched, 1);
+    // the claim's round trip overlaps staging and conv1: it is published in
+    // LDS only before conv1's closing barrier
+    int claim = 0;
+    if (sched && tid == 0) claim = atomicAdd(sched, 1);
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
     const int y0 = ty * 16, x0 = tx * BW;
     __syncthreads();  // previous tile's readers of sin(=c2) and ostg(=c1) are done
+    STEM_STAMP(0);
 
     // ---- A: normalised 16-bit input over (y0-3 .. y0+18) x (x0-3 .. x0+34);
     // out-of-image pixels were fetched as 0 (zero padding in normalised space)
@@ -269,6 +290,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       }
     }
     __syncthreads();
+    STEM_STAMP(1);
     // interior boxes (no receptive field pixel outside the image) skip the zeroing
     const bool interior = ty > 0 && ty < IMG / 16 - 1 && tx > 0 && tx < TPR - 1;
 
@@ -278,19 +300,33 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) w1f[ks][ct] = *(const u16x8*)(sw1 + (ct * 16 + r16) * W1P + ks * 32 + g * 8);
+    // All of this wave's row tiles at once (waves 5-7 own five, the sixth is a
+    // dummy over in_off's tile-0 slots, computed and not stored): reads, then
+    // MFMAs, then the epilogue writes, so neither the LDS read latency nor the
+    // MFMA -> store chain of one tile waits on the previous tile's (the c1
+    // writes would otherwise pin every later sin read behind them).
+    u16x8 pin[N1][2];
+#pragma unroll
+    for (int i = 0; i < N1; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) pin[i][ks] = *(const u16x8*)(sin + in_off[i][ks]);
+    f32x4 acc1[N1][2];
+#pragma unroll
+    for (int i = 0; i < N1; ++i) {
+      acc1[i][0] = bt1[0];
+      acc1[i][1] = bt1[1];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < N1; ++i)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc1[i][ct] = T::mfma(w1f[ks][ct], pin[i][ks], acc1[i][ct]);
 #pragma unroll
     for (int i = 0; i < N1; ++i) {
       const int rt = wave + 8 * i;
-      if (rt >= RT1) break;
-      f32x4 acc[2] = {bt1[0], bt1[1]};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const u16x8 p = *(const u16x8*)(sin + in_off[i][ks]);
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct) acc[ct] = T::mfma(w1f[ks][ct], p, acc[ct]);
-      }
-      bool inside = true;
-      if (!interior) {
+      bool inside = rt < RT1;
+      if (!interior && inside) {
         const int m = rt * 16 + r16;
         const int cy = m / C1W, cx = m - (m / C1W) * C1W;
         inside = (unsigned)(y0 - 2 + cy) < (unsigned)IMG && (unsigned)(x0 - 2 + cx) < (unsigned)IMG;
@@ -299,13 +335,15 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       for (int ct = 0; ct < 2; ++ct) {
         f32x4 r;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) r[j] = relu(acc[ct][j]);
+        for (int j = 0; j < 4; ++j) r[j] = relu(acc1[i][ct][j]);
         u16x4 o = T::pack4(r);
         if (!inside) o = (u16x4)0;
-        *(u16x4*)(c1 + c1_wr[i] + ct * 2 * P1 * 8) = o;
+        if (rt < RT1) *(u16x4*)(c1 + c1_wr[i] + ct * 2 * P1 * 8) = o;
       }
     }
+    if (sched && tid == 0) s_tile[(j + 1) & 1] = claim;
     __syncthreads();
+    STEM_STAMP(2);
 
     const int next = sched ? s_tile[(j + 1) & 1] : tile + gridDim.x;
     fetch(next);  // next box's pixels land while conv2/conv3 run
@@ -343,6 +381,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       }
     }
     __syncthreads();
+    STEM_STAMP(3);
 
     // ---- D: conv3 over the 16x32 box, window-major, 2x2 max-pool in registers
     {
@@ -363,6 +402,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         }
     }
     __syncthreads();
+    STEM_STAMP(4);
     {  // 128 pooled pixels x 4 16-byte channel quarters = 512 threads
       const int w = tid >> 2, q = tid & 3;
       const int wy = w >> 4, wx = w & 15;
