@@ -35,8 +35,10 @@ def _flags():
             f"-I{CSRC}", f"-I{INCLUDE}"]
 
 
-# Per-file extra flags (none needed at present).
-FILE_FLAGS: dict = {}
+# Per-file extra flags.  stem224.hip: no wave-level atomic aggregation, whose
+# prefix-sum code needs the box-claim atomic's return value at once (an
+# s_waitcnt vmcnt(0) at every box start); plain, its wait sits at the use.
+FILE_FLAGS: dict = {"stem224.hip": ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]}
 
 
 def _headers_mtime() -> float:

@@ -38,6 +38,11 @@ __device__ __forceinline__ void win_pixel(int m, int& py, int& px) {
   px = 2 * wx + (sub & 1);
 }
 
+// Workgroup barrier that orders LDS only: this wave's LDS accesses retire
+// first (lgkmcnt(0)), its global stores and prefetch loads stay in flight
+// (__syncthreads' fence would wait for them: vmcnt(0) every phase).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // The nine taps of one 3x3 conv stage over NT row tiles per wave,
 // software-pipelined: tap t multiplies fragments read during tap t-1, and
 // right behind each row tile's two MFMAs that tile's fragment for tap t+1 is
@@ -90,14 +95,14 @@ constexpr float kNormStd[3] = {0.229f, 0.224f, 0.225f};   // cvit_prediction.py:
 
 // Phase stamps (wave 0, per box, after each barrier) for tools/ubench/stem_ubench.hip only.
 #ifdef STEM_STAMPS
-__device__ unsigned long long stem_st[4][32][5];
+__device__ unsigned long long stem_st[4][32][8][7];
 #define STEM_STAMP(k)                                                                          \
   do {                                                                                         \
     __builtin_amdgcn_sched_barrier(0);                                                         \
     unsigned long long t_;                                                                     \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
     __builtin_amdgcn_sched_barrier(0);                                                         \
-    if (blockIdx.x < 4 && tid == 0 && j < 32) stem_st[blockIdx.x][j][(k)] = t_;               \
+    if (blockIdx.x < 4 && lane == 0 && j < 32) stem_st[blockIdx.x][j][wave][(k)] = t_;         \
   } while (0)
 #else
 #define STEM_STAMP(k) \
@@ -208,13 +213,18 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   // Raw input pixels of a box's 22x38 receptive field (pixel tid and
   // tid+512 of it), fetched one box ahead (during conv2/conv3 of the previous
   // box) so phase A never waits on HBM.
-  float raw[2][3];  // U8: the byte values; F32: normalised floats
+  // U8: the byte values, kept as integers until phase A (a conversion here
+  // would make every wave wait for the loads right after issuing them);
+  // F32: normalised floats
+  uint32_t raw01[2], raw2[2];  // U8: channels 0|1 (one 2-byte load), channel 2
+  float raw[2][3];
   bool raw_in[2];
   auto fetch = [&](int tile) {
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
+      raw01[k] = raw2[k] = 0;
       raw[k][0] = raw[k][1] = raw[k][2] = 0.f;
       raw_in[k] = false;
       const int p = tid + 512 * k;
@@ -225,9 +235,10 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       raw_in[k] = true;
       if constexpr (U8) {
         const uint8_t* src = (const uint8_t*)in_ + (((size_t)b * IMG + y) * IMG + x) * 3;
-        raw[k][0] = (float)src[0];
-        raw[k][1] = (float)src[1];
-        raw[k][2] = (float)src[2];
+        uint16_t v01;
+        __builtin_memcpy(&v01, src, 2);
+        raw01[k] = v01;
+        raw2[k] = src[2];
       } else {
         const float* src = (const float*)in_ + (size_t)b * 3 * IMG * IMG + (size_t)y * IMG + x;
         raw[k][0] = src[0];
@@ -261,7 +272,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
     const int y0 = ty * 16, x0 = tx * BW;
-    __syncthreads();  // previous tile's readers of sin(=c2) and ostg(=c1) are done
+    lds_barrier();  // previous tile's readers of sin(=c2) and ostg(=c1) are done
     STEM_STAMP(0);
 
     // ---- A: normalised 16-bit input over (y0-3 .. y0+18) x (x0-3 .. x0+34);
@@ -272,9 +283,9 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       if (p < IN_PIX) {
         u16x4 h;
         if constexpr (U8) {
-          h[0] = raw_in[k] ? lut[(int)raw[k][0]] : (uint16_t)0;
-          h[1] = raw_in[k] ? lut[256 + (int)raw[k][1]] : (uint16_t)0;
-          h[2] = raw_in[k] ? lut[512 + (int)raw[k][2]] : (uint16_t)0;
+          h[0] = raw_in[k] ? lut[raw01[k] & 255] : (uint16_t)0;
+          h[1] = raw_in[k] ? lut[256 + (raw01[k] >> 8)] : (uint16_t)0;
+          h[2] = raw_in[k] ? lut[512 + raw2[k]] : (uint16_t)0;
         } else {
           h[0] = T::from_f32(raw[k][0]);
           h[1] = T::from_f32(raw[k][1]);
@@ -289,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         if (ix == IW - 1) *(u16x4*)(sin + p * 8 + 4) = (u16x4)0;
       }
     }
-    __syncthreads();
+    lds_barrier();
     STEM_STAMP(1);
     // interior boxes (no receptive field pixel outside the image) skip the zeroing
     const bool interior = ty > 0 && ty < IMG / 16 - 1 && tx > 0 && tx < TPR - 1;
@@ -342,7 +353,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       }
     }
     if (sched && tid == 0) s_tile[(j + 1) & 1] = claim;
-    __syncthreads();
+    lds_barrier();
     STEM_STAMP(2);
 
     const int next = sched ? s_tile[(j + 1) & 1] : tile + gridDim.x;
@@ -360,6 +371,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         acc[i][1] = bt2[1];
       }
       tap_pipeline<T, true, N2, RP>(acc, c1, c2_rd, sw2 + (g * 32 + r16) * 8);
+      STEM_STAMP(5);
 #pragma unroll
       for (int i = 0; i < N2; ++i) {
         const int m = (wave + 8 * i) * 16 + r16;
@@ -380,7 +392,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     STEM_STAMP(3);
 
     // ---- D: conv3 over the 16x32 box, window-major, 2x2 max-pool in registers
@@ -392,6 +404,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         acc[i][1] = bn3[1];
       }
       tap_pipeline<T, false, 4, RP>(acc, c2, c3_rd, sw3 + (g * 32 + r16) * 8);
+      STEM_STAMP(6);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
           ostg[((wave * 4 + i) * 4 + g) * 40 + ct * 16 + r16] = T::from_f32(relu(mx));
         }
     }
-    __syncthreads();
+    lds_barrier();
     STEM_STAMP(4);
     {  // 128 pooled pixels x 4 16-byte channel quarters = 512 threads
       const int w = tid >> 2, q = tid & 3;

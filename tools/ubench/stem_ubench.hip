@@ -1,7 +1,7 @@
 // Phase timeline of the fused stem kernel (stem224.hip) from s_memtime
 // stamps taken by wave 0 right after each of the five per-box barriers.
 // GPU box:
-//   hipcc --offload-arch=gfx950 -O3 -DSTEM_STAMPS -I fac_fake_amd/csrc -I include \
+//   hipcc --offload-arch=gfx950 -O3 -mllvm -amdgpu-atomic-optimizer-strategy=None -DSTEM_STAMPS -I fac_fake_amd/csrc -I include \
 //     -o /tmp/stem_ubench tools/ubench/stem_ubench.hip && /tmp/stem_ubench
 #include "../../fac_fake_amd/csrc/stem224.hip"
 
@@ -44,16 +44,25 @@ int main() {
     (void)hipEventElapsedTime(&ms, e0, e1);
   }
   printf("stem224 B=%d: %.1f us\n", B, ms * 1e3);
-  unsigned long long st[4][32][5];
+  static unsigned long long st[4][32][8][7];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(fac::stem_st), sizeof(st));
   const char* nm[5] = {"A stage", "B conv1", "C conv2", "D conv3", "out"};
   for (int wg = 0; wg < 2; ++wg) {
+    printf("wg %d: mean s_memtime ticks per box, phase = barrier to barrier (wave 0):", wg);
     double sum[5] = {0};
     int n = 0;
     for (int j = 1; j < 31; ++j, ++n)
-      for (int k = 0; k < 5; ++k) sum[k] += (double)((k < 4 ? st[wg][j][k + 1] : st[wg][j + 1][0]) - st[wg][j][k]);
-    printf("wg %d mean s_memtime ticks per box from the barrier before:", wg);
+      for (int k = 0; k < 5; ++k) sum[k] += (double)((k < 4 ? st[wg][j][0][k + 1] : st[wg][j + 1][0][0]) - st[wg][j][0][k]);
     for (int k = 0; k < 5; ++k) printf("  %s %.0f", nm[k], sum[k] / n);
+    printf("\n  per wave, barrier -> end of taps: conv2 / conv3:");
+    for (int w = 0; w < 8; ++w) {
+      double t2 = 0, t3 = 0;
+      for (int j = 1; j < 31; ++j) {
+        t2 += (double)(st[wg][j][w][5] - st[wg][j][0][2]);
+        t3 += (double)(st[wg][j][w][6] - st[wg][j][0][3]);
+      }
+      printf("  w%d %.0f/%.0f", w, t2 / n, t3 / n);
+    }
     printf("\n");
   }
   return 0;
