@@ -95,7 +95,7 @@ constexpr float kNormStd[3] = {0.229f, 0.224f, 0.225f};   // cvit_prediction.py:
 
 // Phase stamps (wave 0, per box, after each barrier) for tools/ubench/stem_ubench.hip only.
 #ifdef STEM_STAMPS
-__device__ unsigned long long stem_st[4][32][8][7];
+__device__ unsigned long long stem_st[4][32][8][8];
 #define STEM_STAMP(k)                                                                          \
   do {                                                                                         \
     __builtin_amdgcn_sched_barrier(0);                                                         \
@@ -333,6 +333,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       for (int i = 0; i < N1; ++i)
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) acc1[i][ct] = T::mfma(w1f[ks][ct], pin[i][ks], acc1[i][ct]);
+    STEM_STAMP(7);
 #pragma unroll
     for (int i = 0; i < N1; ++i) {
       const int rt = wave + 8 * i;

@@ -44,7 +44,7 @@ int main() {
     (void)hipEventElapsedTime(&ms, e0, e1);
   }
   printf("stem224 B=%d: %.1f us\n", B, ms * 1e3);
-  static unsigned long long st[4][32][8][7];
+  static unsigned long long st[4][32][8][8];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(fac::stem_st), sizeof(st));
   const char* nm[5] = {"A stage", "B conv1", "C conv2", "D conv3", "out"};
   for (int wg = 0; wg < 2; ++wg) {
@@ -54,6 +54,12 @@ int main() {
     for (int j = 1; j < 31; ++j, ++n)
       for (int k = 0; k < 5; ++k) sum[k] += (double)((k < 4 ? st[wg][j][0][k + 1] : st[wg][j + 1][0][0]) - st[wg][j][0][k]);
     for (int k = 0; k < 5; ++k) printf("  %s %.0f", nm[k], sum[k] / n);
+    printf("\n  per wave, barrier -> end of conv1 MFMAs:");
+    for (int w = 0; w < 8; ++w) {
+      double t1 = 0;
+      for (int j = 1; j < 31; ++j) t1 += (double)(st[wg][j][w][7] - st[wg][j][0][1]);
+      printf("  w%d %.0f", w, t1 / n);
+    }
     printf("\n  per wave, barrier -> end of taps: conv2 / conv3:");
     for (int w = 0; w < 8; ++w) {
       double t2 = 0, t3 = 0;
