@@ -47,6 +47,8 @@ SIGNATURES = {
     "fac_profile_forward_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int,
                                               ctypes.c_void_p]),
+    "fac_stem_event_ms": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                         ctypes.POINTER(ctypes.c_int)]),
     "fac_check_device_errors": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     "fac_video_score": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_crop_resize_u8": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,

@@ -134,6 +134,11 @@ struct fac_ctx {
   int* errflag = nullptr;
   int* sched = nullptr;  // 2 ints: stem224 dynamic box counter + finished-workgroup count
   int stem_dynamic = 1;  // option "stem_dynamic": stem224 claims boxes from `sched` (else static)
+  // option "stem_events": hipEvent pairs around every fused-stem launch (the
+  // bench's timed region), read back by fac_stem_event_ms
+  bool stem_ev = false;
+  std::vector<hipEvent_t> stem_evs;
+  size_t stem_ev_used = 0;
   uint16_t* zero16 = nullptr;  // 256 zero bytes: the source of zero-padding glds pieces
 };
 
@@ -464,8 +469,21 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     bool copied = false;  // stop_after's output already copied for this chunk
     if (c->fuse_stem224 && (stop_after < 0 || stop_after >= 2)) {
       // conv1..conv3 + pool in one kernel; the profile reports it as stage 0 (conv1)
+      hipEvent_t sev0 = nullptr, sev1 = nullptr;
+      if (c->stem_ev) {
+        while (c->stem_evs.size() < c->stem_ev_used + 2) {
+          hipEvent_t e;
+          HIP_TRY(c, hipEventCreate(&e));
+          c->stem_evs.push_back(e);
+        }
+        sev0 = c->stem_evs[c->stem_ev_used];
+        sev1 = c->stem_evs[c->stem_ev_used + 1];
+        c->stem_ev_used += 2;
+        HIP_TRY(c, hipEventRecord(sev0, st));
+      }
       HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_wp, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
                                 c->conv[1].b, cur, nb, c->num_cu, st, c->stem_dynamic ? c->sched : nullptr));
+      if (sev1) HIP_TRY(c, hipEventRecord(sev1, st));
       MARK(0);
       l0 = 2;
       if (stop_after == 2) {
@@ -642,6 +660,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     c->fuse_stem224 = value != 0;
     return FAC_OK;
   }
+  if (k == "stem_events") {
+    c->stem_ev = value != 0;
+    c->stem_ev_used = 0;
+    return FAC_OK;
+  }
   if (k == "stem_dynamic") {
     c->stem_dynamic = value != 0;
     return FAC_OK;
@@ -798,6 +821,24 @@ int fac_profile_forward_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t
   return rc;
 }
 
+int fac_stem_event_ms(fac_ctx* c, float* avg_ms, int* n_launches) {
+  if (!c || !avg_ms || !n_launches) return FAC_ERR_ARG;
+  DevGuard g(c->device);
+  *avg_ms = 0.f;
+  *n_launches = (int)(c->stem_ev_used / 2);
+  if (!*n_launches) return FAC_OK;
+  HIP_TRY(c, hipEventSynchronize(c->stem_evs[c->stem_ev_used - 1]));
+  double sum = 0.0;
+  for (size_t i = 0; i < c->stem_ev_used; i += 2) {
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->stem_evs[i], c->stem_evs[i + 1]));
+    sum += ms;
+  }
+  *avg_ms = (float)(sum / *n_launches);
+  c->stem_ev_used = 0;
+  return FAC_OK;
+}
+
 int fac_check_device_errors(fac_ctx* c, int* flags) {
   if (!c || !flags) return FAC_ERR_ARG;
   *flags = 0;
@@ -828,6 +869,7 @@ void fac_destroy(fac_ctx* c) {
         (void)hipEventDestroy(c->ev_tail[i]);
       }
     }
+    for (hipEvent_t e : c->stem_evs) (void)hipEventDestroy(e);
     for (void* p : c->weights) (void)hipFree(p);
     if (c->ws) (void)hipFree(c->ws);
   }

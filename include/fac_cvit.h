@@ -137,6 +137,12 @@ int fac_debug_gemm(fac_ctx* ctx, int epi, const uint16_t* d_a, const uint16_t* d
 int fac_profile_forward_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
                            float* stage_ms, int n_stages, void* stream);
 
+/* Mean duration of the fused-stem launches recorded since option
+ * "stem_events" was set (hipEvent pairs on the launching stream), and their
+ * count; resets the record.  The bench's roofline for the stem kernel is
+ * taken over its timed region with this. */
+int fac_stem_event_ms(fac_ctx* ctx, float* avg_ms, int* n_launches);
+
 /* Nonzero if a previous forward saw a pos_index outside [0,32) (clamped).
  * Synchronises the context's device; not for use inside graph capture. */
 int fac_check_device_errors(fac_ctx* ctx, int* flags);
@@ -164,7 +170,8 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * "gemm_patch" / "gemm_qkv" / "gemm_out" / "gemm_ff1" / "gemm_ff2" /
  * "gemm_head" (GEMM tile variant -1..3 per call site), "proj_splits" (split-K
  * of to_out and FF2: 1, 2 or 4), "tail_only" (before fac_load_weights: no
- * conv stem, fac_forward_features only), "tail_priority", "stem_dynamic" (1 =
+ * conv stem, fac_forward_features only), "tail_priority", "stem_events" (1 =
+ * time every fused-stem launch, fac_stem_event_ms), "stem_dynamic" (1 =
  * the fused stem claims boxes from a device counter, the default; 0 = static
  * box schedule), "ffn_ln_eps_exp" (n:
  * the FeedForward PreNorm LayerNorm uses eps = 10^-n; default 5, the RepBn8
