@@ -39,10 +39,14 @@ void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* ou
   for (int nb = 0; nb < co / BN; ++nb)
     for (int ch = 0; ch < nch; ++ch)
       for (int t = 0; t < 9; ++t)
-        for (int qq = 0; qq < CK / 8; ++qq)
+        for (int qq = 0; qq < CK / 8; ++qq) {
+          // 112x112 layers: conv.hip's pixel-major halo hands lane group qq
+          // channel piece qq ^ 2 on odd kernel rows (its PM comment)
+          const int qs = (H == 112 && (t / 3) % 2 == 1) ? qq ^ 2 : qq;
           for (int nl = 0; nl < BN; ++nl)
             for (int j = 0; j < 8; ++j)
-              out[q++] = to16(dtype, w[((size_t)(nb * BN + nl) * ci + ch * CK + qq * 8 + j) * 9 + t]);
+              out[q++] = to16(dtype, w[((size_t)(nb * BN + nl) * ci + ch * CK + qs * 8 + j) * 9 + t]);
+        }
 }
 
 // stem224's conv1 K order: k = ((ky*2 + kx/2)*2 + kx%2)*4 + cin (kx = 3 and
