@@ -97,19 +97,21 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // The halo image is filled by global_load_lds, one 64-slot wave
   // instruction at a time; pad it to whole instructions, a multiple of 4 so
   // every wave issues the same number (HPW).
-  // PM (the 112x112 layers: 16x16 boxes, BN 64): pixel-major halo image
-  // [hy][hx][4 x 16 B] without row padding, the 16-byte piece index
-  // XOR-swizzled by row parity (position j of pixel (hy,hx) holds channel
-  // piece j ^ 2*(hy&1)).  Each glds wave instruction then reads 16
+  // PM (every layer but the 224x224 ones, whose packed weights stem224.hip
+  // shares): pixel-major halo image [hy][RPX][4 x 16 B], the 16-byte piece
+  // index XOR-swizzled by row parity (position j of pixel (hy,hx) holds
+  // channel piece j ^ 2*(hy&1)).  Each glds wave instruction then reads 16
   // consecutive halo pixels' 64 contiguous bytes (a q-major image's
   // instructions touch 64 pixels, i.e. 64 cache lines, for 16 bytes each), and
-  // the fragment reads stay conflict-free for every tap (simulated over the
-  // ds_read_b128 lane groups).  Lane group g always reads position
-  // g ^ 2*(py&1), so on odd kernel rows it holds channel piece g ^ 2: the
-  // weight packing swaps pieces q <-> q^2 of those taps to match
-  // (pack_conv3x3, stack_ops.hip) -- a permutation of the MFMA's k order.
-  constexpr bool PM = TH == 16 && TW == 16 && BN == 64;
-  constexpr int HSLOTS = PM ? (HH * HWD * 4 + 255) / 256 * 256 : (4 * NHP + 255) / 256 * 256;
+  // the fragment reads are conflict-free for every tap (simulated over the
+  // ds_read_b128 lane groups; 14x14 boxes with RPX = 17: 1.08-way, q-major
+  // 1.4).  Lane group g always reads position g ^ 2*(py&1), so on odd kernel
+  // rows it holds channel piece g ^ 2: the weight packing swaps pieces
+  // q <-> q^2 of those taps to match (pack_conv3x3, stack_ops.hip) -- a
+  // permutation of the MFMA's k order.
+  constexpr bool PM = !(TH == 16 && TW == 16 && BN == 32);
+  constexpr int RPX = TW == 14 ? HWD + 1 : HWD;  // halo row pitch (pixels)
+  constexpr int HSLOTS = PM ? (HH * RPX * 4 + 255) / 256 * 256 : (4 * NHP + 255) / 256 * 256;
   constexpr int HPW = HSLOTS / 256;
   constexpr int HALO = HSLOTS * 8;          // elements per halo buffer
   constexpr int WSL = BN * CK;              // elements per tap slice
@@ -153,8 +155,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
     int q, hy, hx;
     if constexpr (PM) {
       const int pix = slot >> 2;
-      hy = pix / HWD;
-      hx = pix - (pix / HWD) * HWD;
+      hy = pix / RPX;
+      hx = pix - (pix / RPX) * RPX;
       q = hy < HH ? (slot & 3) ^ ((hy & 1) << 1) : 4;
     } else {
       q = slot / NHP;
@@ -166,6 +168,10 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
     hsrc[i] = -1;
     if (q < 4 && hy < HH && hx < HWD && y >= 0 && y < H && x >= 0 && x < W) hsrc[i] = (y * W + x) * Cin + q * 8;
   }
+  // (the 112x112 pooled variant spills one map entry at its 128-VGPR budget:
+  // the store sits in the prologue and the reload at a chunk start, both
+  // outside the counted-vmcnt steps; recomputing the map per chunk instead
+  // measured slower, conv5 272 -> 286 us)
   auto issue_halo = [&](uint16_t* dst, int c) {
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
@@ -198,7 +204,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
     if (m >= NPIX) m = 0;  // padding rows: computed on pixel 0, never stored
     int py, px;
     box_pixel<TW>(m, py, px);
-    abase[rt] = PM ? ((py * HWD + px) * 4 + ((lane >> 4) ^ ((py & 1) << 1))) * 8
+    abase[rt] = PM ? ((py * RPX + px) * 4 + ((lane >> 4) ^ ((py & 1) << 1))) * 8
                    : ((lane >> 4) * NHP + py * HALO_RP + px) * 8;
   }
   int bbase[CTW];
@@ -280,7 +286,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
         for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
       }
       constexpr int kyn = t < 8 ? (t + 1) / 3 : 0, kxn = t < 8 ? (t + 1) % 3 : 0;
-      constexpr int ntoff = PM ? (kyn * HWD + kxn) * 32 : (kyn * HALO_RP + kxn) * 8;
+      constexpr int ntoff = PM ? (kyn * RPX + kxn) * 32 : (kyn * HALO_RP + kxn) * 8;
       const uint16_t* hnx = t < 8 ? hb : hbn;
       const uint16_t* wbn = wring + ((t + 1) % 3) * WSL;
 #pragma unroll

@@ -40,9 +40,9 @@ void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* ou
     for (int ch = 0; ch < nch; ++ch)
       for (int t = 0; t < 9; ++t)
         for (int qq = 0; qq < CK / 8; ++qq) {
-          // 112x112 layers: conv.hip's pixel-major halo hands lane group qq
+          // below 224x224: conv.hip's pixel-major halo hands lane group qq
           // channel piece qq ^ 2 on odd kernel rows (its PM comment)
-          const int qs = (H == 112 && (t / 3) % 2 == 1) ? qq ^ 2 : qq;
+          const int qs = (H != 224 && (t / 3) % 2 == 1) ? qq ^ 2 : qq;
           for (int nl = 0; nl < BN; ++nl)
             for (int j = 0; j < 8; ++j)
               out[q++] = to16(dtype, w[((size_t)(nb * BN + nl) * ci + ch * CK + qs * 8 + j) * 9 + t]);
