@@ -315,9 +315,14 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       }
       // Retire slice s+1 (and at t = 1 the next halo), leaving younger glds in
       // flight; wait + barrier in ONE asm statement, so no LDS access can be
-      // scheduled between this wave's wait and the workgroup barrier.
+      // scheduled between this wave's wait and the workgroup barrier.  The LDS
+      // wait retires this step's weight-fragment reads (the ring slot the next
+      // step refills) and leaves the youngest ones, the A-fragment prefetches
+      // for the next tap (halo buffers, not rewritten here), in flight: L of
+      // them (with PB, A(0) sits in one group with the bnx reads).
       constexpr int N = WPW + (HB == 2 && t <= 1 ? HPW : 0);
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+      constexpr int L = (HB == 2 || t < 8) ? (PB ? RTW - 1 : RTW) : 0;
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(%1)\n\ts_barrier" ::"n"(N), "n"(L) : "memory");
       __builtin_amdgcn_sched_barrier(0);
     };
     step(std::integral_constant<int, 0>{});
