@@ -272,26 +272,33 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
     const int y0 = ty * 16, x0 = tx * BW;
+    // ---- A: normalised 16-bit input over (y0-3 .. y0+18) x (x0-3 .. x0+34);
+    // out-of-image pixels were fetched as 0 (zero padding in normalised space).
+    // The LUT lookups go before the box barrier (the LUT is never rewritten),
+    // so their latency overlaps the wait for the previous box's last readers.
+    u16x4 hv[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      u16x4 h;
+      if constexpr (U8) {
+        h[0] = raw_in[k] ? lut[raw01[k] & 255] : (uint16_t)0;
+        h[1] = raw_in[k] ? lut[256 + (raw01[k] >> 8)] : (uint16_t)0;
+        h[2] = raw_in[k] ? lut[512 + raw2[k]] : (uint16_t)0;
+      } else {
+        h[0] = T::from_f32(raw[k][0]);
+        h[1] = T::from_f32(raw[k][1]);
+        h[2] = T::from_f32(raw[k][2]);
+      }
+      h[3] = 0;
+      hv[k] = h;
+    }
     lds_barrier();  // previous tile's readers of sin(=c2) and ostg(=c1) are done
     STEM_STAMP(0);
-
-    // ---- A: normalised 16-bit input over (y0-3 .. y0+18) x (x0-3 .. x0+34);
-    // out-of-image pixels were fetched as 0 (zero padding in normalised space)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int p = tid + 512 * k;
       if (p < IN_PIX) {
-        u16x4 h;
-        if constexpr (U8) {
-          h[0] = raw_in[k] ? lut[raw01[k] & 255] : (uint16_t)0;
-          h[1] = raw_in[k] ? lut[256 + (raw01[k] >> 8)] : (uint16_t)0;
-          h[2] = raw_in[k] ? lut[512 + raw2[k]] : (uint16_t)0;
-        } else {
-          h[0] = T::from_f32(raw[k][0]);
-          h[1] = T::from_f32(raw[k][1]);
-          h[2] = T::from_f32(raw[k][2]);
-        }
-        h[3] = 0;
+        const u16x4 h = hv[k];
         // pixel-pair slot p = (pixel p, pixel p+1): left half of slot p, right
         // half of slot p-1 (the last column's right half: zeros, zero weight)
         const int ix = p - (p / IW) * IW;
