@@ -464,3 +464,32 @@ def test_video_driver_matches_drop_in(models, mode):
     assert torch.equal(logits.cpu(), ref)
     assert score == float(pre_process_prediction(pred_sig(ref)))
 
+
+
+def test_stem_event_timing(models):
+    """Option stem_events (the bench's roofline source): fac_stem_event_ms
+    reports one timed launch per pipelined forward, then resets."""
+    import ctypes
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models["bf16"]
+    ctx = m._ctx
+    x = torch.from_numpy(make_crops(64, seed=5)).to(DEV)
+    p = (torch.arange(64, device=DEV) % 32).to(torch.int32)
+    lg = torch.empty(64, 2, device=DEV)
+    s = torch.cuda.Stream(DEV)
+    m.set_option("stem_events", 1)
+    try:
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                _lib.check(lib.fac_forward_nhwc_u8_pipelined(ctx, x.data_ptr(), 64, p.data_ptr(), lg.data_ptr(), None,
+                                                             None, s.cuda_stream), ctx, "pipelined")
+            _lib.check(lib.fac_pipeline_join(ctx, 0, s.cuda_stream), ctx, "join")
+        avg, n = ctypes.c_float(), ctypes.c_int()
+        _lib.check(lib.fac_stem_event_ms(ctx, ctypes.byref(avg), ctypes.byref(n)), ctx, "stem_event_ms")
+        assert n.value == 3 and 0.0 < avg.value < 100.0, (n.value, avg.value)
+        _lib.check(lib.fac_stem_event_ms(ctx, ctypes.byref(avg), ctypes.byref(n)), ctx, "stem_event_ms")
+        assert n.value == 0
+    finally:
+        m.set_option("stem_events", 0)
+    torch.cuda.synchronize()
