@@ -257,11 +257,9 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   // thread 0 overwrites it.  The last workgroup out resets the counters.
   __shared__ int s_tile[2];
   int tile = blockIdx.x;
-  if (sched) {
-    if (tid == 0) s_tile[0] = atomicAdd(sched, 1);
-    __syncthreads();
-    tile = s_tile[0];
-  }
+  if (sched && tid == 0) s_tile[0] = atomicAdd(sched, 1);
+  __syncthreads();  // LUT and weights written (the first box reads the LUT before its barrier), claim published
+  if (sched) tile = s_tile[0];
   fetch(tile);
 
   for (int j = 0; tile < ntiles; ++j) {
