@@ -125,3 +125,26 @@ def test_sharding_bounds():
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             sizes = [hi - lo for lo, hi in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("H,ci,co", [(224, 32, 32), (112, 64, 64), (56, 128, 128), (28, 256, 256), (14, 512, 512)])
+def test_conv3x3_weight_packing_layout(built_lib, H, ci, co):
+    """fac_conv3x3_pack (host code, stack_ops.hip): [n-block][chunk][tap][q][BN][8]
+    with BN = conv_block_n(H); below 224 the 16-byte pieces of the odd-kernel-row
+    taps are stored as q ^ 2, matching conv.hip's row-parity-swizzled halo."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    bn = {224: 32, 112: 64, 56: 128, 28: 256, 14: 128}[H]
+    n = lib.fac_conv3x3_packed_elems(H, ci, co)
+    assert n == co * ci * 9
+    w = (torch.arange(co * ci * 9, dtype=torch.float32) % 2039).reshape(co, ci, 3, 3) / 1024.0
+    out = torch.empty(n, dtype=torch.int16)
+    _lib.check(lib.fac_conv3x3_pack(1, H, ci, co, w.data_ptr(), out.data_ptr()), None, "pack")  # fp16: exact here
+    got = out.view(torch.float16).float().reshape(co // bn, ci // 32, 9, 4, bn, 8)
+    for nb in range(co // bn):
+        for ch in range(ci // 32):
+            for t in range(9):
+                for q in range(4):
+                    qs = q ^ 2 if (H != 224 and (t // 3) % 2 == 1) else q
+                    want = w[nb * bn:(nb + 1) * bn, ch * 32 + qs * 8:ch * 32 + qs * 8 + 8].reshape(bn, 8, 9)[:, :, t]
+                    assert torch.equal(got[nb, ch, t, q], want), (nb, ch, t, q)
