@@ -186,6 +186,11 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
   constexpr int QPR = BN / 8;                 // 8-channel pieces per row
   constexpr int QPT = BM * QPR / NT;          // pieces per thread
   const bool resid = p.flags & FAC_CONV_RESID;
+  // all bias values first (one wait for the lot, not one round trip per
+  // channel tile), then the residual vectors
+  float bvs[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) bvs[ct] = p.bias ? p.bias[n0 + wn * WTN + ct * 16 + (lane & 15)] : 0.f;
   u16x8 rv[QPT];
 #pragma unroll
   for (int i = 0; i < QPT; ++i) {
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     const int col = wn * WTN + ct * 16 + (lane & 15);
-    const float bv = p.bias ? p.bias[n0 + col] : 0.f;
+    const float bv = bvs[ct];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
