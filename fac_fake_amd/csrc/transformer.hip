@@ -113,10 +113,15 @@ __global__ __launch_bounds__(256, NS <= 3 ? 2 : 1) void gemm_nt(const uint16_t* 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy tiles
 
+  // all bias values in flight at once (one wait, not a round trip per tile column)
+  float bvs[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+    bvs[j] = (EPI == EPI_PARTIAL || bias == nullptr) ? 0.f : bias[n0 + wn * (BN / WN) + j * 16 + (lane & 15)];
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-    const float bv = (EPI == EPI_PARTIAL || bias == nullptr) ? 0.f : bias[n];
+    const float bv = bvs[j];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
