@@ -46,6 +46,27 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
+def _check_conv_waits(compile_fn, verbose: bool) -> None:
+    """The conv kernels' relaxed per-tap LDS waits are sound only for the
+    issue order the compiler chose (isa_check.py).  Verify it on the fresh
+    object; if any wait fails, rebuild conv.hip with every wait strict."""
+    from . import isa_check
+    obj = OBJDIR / "conv.o"
+    rep = isa_check.check_objects([obj], arch=ARCH)
+    if verbose:
+        print(f"isa_check: {rep.kernels} conv kernels, {rep.waits} relaxed LDS waits, "
+              f"{len(rep.problems)} problems", file=sys.stderr)
+    if rep.ok:
+        return
+    print("isa_check: relaxed LDS waits unsound in this build, rebuilding conv.hip with "
+          "FAC_CONV_STRICT_LGKM:\n  " + "\n  ".join(rep.problems[:8]), file=sys.stderr)
+    FILE_FLAGS["conv.hip"] = FILE_FLAGS.get("conv.hip", []) + ["-DFAC_CONV_STRICT_LGKM"]
+    compile_fn((CSRC / "conv.hip", obj))
+    rep = isa_check.check_objects([obj], arch=ARCH)
+    if not rep.ok:
+        raise RuntimeError("isa_check failed even with strict LDS waits:\n" + "\n".join(rep.problems[:8]))
+
+
 def build(verbose: bool = False, force: bool = False) -> Path:
     """Compile every csrc/*.hip for gfx950 and link libfac_cvit.so."""
     hipcc = _hipcc()
@@ -70,6 +91,8 @@ def build(verbose: bool = False, force: bool = False) -> Path:
 
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(_compile, jobs))
+    if any(s.name == "conv.hip" for s, _ in jobs):
+        _check_conv_waits(_compile, verbose)
     objs = [OBJDIR / (s.stem + ".o") for s in srcs]
     if force or jobs or not LIB.exists() or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)]

@@ -321,7 +321,16 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       // for the next tap (halo buffers, not rewritten here), in flight: L of
       // them (with PB, A(0) sits in one group with the bnx reads).
       constexpr int N = WPW + (HB == 2 && t <= 1 ? HPW : 0);
+      // The relaxed wait relies on the issue order; fac_fake_amd/isa_check.py
+      // verifies it on the built code object (each of the L youngest LDS ops
+      // before every such barrier is a ds_read_b128 whose registers next feed
+      // an MFMA's A operand, no scalar-memory op in the step) and rebuilds
+      // this file with FAC_CONV_STRICT_LGKM (L = 0) if any wait fails.
+#ifdef FAC_CONV_STRICT_LGKM
+      constexpr int L = 0;
+#else
       constexpr int L = (HB == 2 || t < 8) ? (PB ? RTW - 1 : RTW) : 0;
+#endif
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(%1)\n\ts_barrier" ::"n"(N), "n"(L) : "memory");
       __builtin_amdgcn_sched_barrier(0);
     };

@@ -14,11 +14,37 @@
 // sum with float weights, so it may differ by one count on exact .5 ties
 // (cv2 is not in the image: parity with it is unpinned).
 // Boxes are clipped to the frame; an empty box gives a zero crop.
+//
+// cv2 averages areas only when neither axis grows.  A box under 224 px on
+// either axis takes cv2's bilinear path with area-mode coefficients on BOTH
+// axes (hal::resize, OpenCV 4.x resize.cpp; restated in oracle/video.py
+// `linear_area_coeffs` / `_resize_linear_area`): source index
+// s = floor(d*scale), fraction (d+1) - (s+1)/scale wrapped to [0,1) in float,
+// taps rounded to 1/2048; a horizontal pass in exact integers and the SIMD
+// vertical pass for uint8 ((D >> 4) mulhi tap, summed, (+2) >> 2).  The
+// coefficient arithmetic is written with explicit _rn intrinsics so nothing is
+// contracted into an FMA: every index and tap is bit-identical to the host's.
 #include "common.hpp"
 
 namespace fac {
 
 constexpr int kCrop = 224;
+
+// cv2's area-mode bilinear coefficients of output pixel d for an n-pixel
+// span: first source index and the two taps in 1/2048 units.
+__device__ inline void linear_area_tap(int d, int n, bool clamp_fraction, int& s, int& a0, int& a1) {
+  const double inv = __ddiv_rn((double)kCrop, (double)n);
+  const double scale = __ddiv_rn(1.0, inv);
+  s = (int)floor(__dmul_rn((double)d, scale));
+  float f = (float)__dsub_rn((double)(d + 1), __dmul_rn((double)(s + 1), inv));
+  f = f <= 0.f ? 0.f : __fsub_rn(f, floorf(f));
+  if (clamp_fraction && s >= n - 1) {
+    s = n - 1;
+    f = 0.f;
+  }
+  a0 = __float2int_rn(__fmul_rn(__fsub_rn(1.f, f), 2048.f));
+  a1 = __float2int_rn(__fmul_rn(f, 2048.f));
+}
 
 // One thread per output pixel (all 3 channels); grid (crop, output row).
 __global__ __launch_bounds__(256) void crop_resize_area_u8(const uint8_t* __restrict__ frames, int n_frames, int H,
@@ -33,6 +59,28 @@ __global__ __launch_bounds__(256) void crop_resize_area_u8(const uint8_t* __rest
   const int nx = x1 - x0, ny = y1 - y0;
   if (f < 0 || f >= n_frames || nx <= 0 || ny <= 0) {
     dst[0] = dst[1] = dst[2] = 0;
+    return;
+  }
+  if (nx < kCrop || ny < kCrop) {
+    int sx, a0, a1, sy, b0, b1;
+    linear_area_tap(ox, nx, true, sx, a0, a1);
+    linear_area_tap(oy, ny, false, sy, b0, b1);
+    const int sx1 = min(sx + 1, nx - 1);  // a1 == 0 whenever this clamps
+    const int r0 = min(max(sy, 0), ny - 1), r1 = min(max(sy + 1, 0), ny - 1);
+    const uint8_t* p0 = frames + (((size_t)f * H + y0 + r0) * W + x0) * 3;
+    const uint8_t* p1 = frames + (((size_t)f * H + y0 + r1) * W + x0) * 3;
+    int v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int d0 = p0[sx * 3 + c] * a0 + p0[sx1 * 3 + c] * a1;  // horizontal pass, exact
+      const int d1 = p1[sx * 3 + c] * a0 + p1[sx1 * 3 + c] * a1;
+      const int h0 = min(d0 >> 4, 32767), h1 = min(d1 >> 4, 32767);
+      const int s = ((h0 * b0) >> 16) + ((h1 * b1) >> 16);
+      v[c] = min(max((s + 2) >> 2, 0), 255);
+    }
+    dst[0] = (uint8_t)v[2];  // BGR -> RGB
+    dst[1] = (uint8_t)v[1];
+    dst[2] = (uint8_t)v[0];
     return;
   }
   // interval of this output pixel in 1/224-pixel units, relative to the box

@@ -140,6 +140,14 @@ struct fac_ctx {
   std::vector<hipEvent_t> stem_evs;
   size_t stem_ev_used = 0;
   uint16_t* zero16 = nullptr;  // 256 zero bytes: the source of zero-padding glds pieces
+  // Conv stacks of one context share the activation buffers and the stem's
+  // box counter (`sched`), so two of them must never overlap: every conv
+  // stack records ev_stack on its stream, and a conv stack enqueued on a
+  // different stream first waits for it.  (Inside a stream capture the
+  // caller orders the graph launches; no external event is waited on there.)
+  hipEvent_t ev_stack = nullptr;
+  hipStream_t stack_st = nullptr;
+  bool stack_rec = false;
 };
 
 namespace {
@@ -432,6 +440,27 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   int rc = ensure_ws(c, B);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  // order this conv stack after the context's previous one (see fac_ctx::ev_stack)
+  struct StackOrder {
+    fac_ctx* c;
+    hipStream_t st;
+    bool active;
+    ~StackOrder() {
+      if (active && hipEventRecord(c->ev_stack, st) == hipSuccess) {
+        c->stack_st = st;
+        c->stack_rec = true;
+      }
+    }
+  } order{c, st, false};
+  if (!stem_in) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(c, hipStreamIsCapturing(st, &cs));
+    if (cs == hipStreamCaptureStatusNone) {
+      if (!c->ev_stack) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_stack, hipEventDisableTiming));
+      if (c->stack_rec && c->stack_st != st) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_stack, 0));
+      order.active = true;
+    }
+  }
   if (!stem_dst) {
     // a synchronous forward shares the encoder workspace with pipelined
     // tails still in flight: order it after them
@@ -870,6 +899,7 @@ void fac_destroy(fac_ctx* c) {
       }
     }
     for (hipEvent_t e : c->stem_evs) (void)hipEventDestroy(e);
+    if (c->ev_stack) (void)hipEventDestroy(c->ev_stack);
     for (void* p : c->weights) (void)hipFree(p);
     if (c->ws) (void)hipFree(c->ws);
   }

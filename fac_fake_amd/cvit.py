@@ -20,8 +20,12 @@ a CPU tensor or a missing library raises.
 
 Extensions beyond the reference: ``pos_index=`` (explicit slot per crop, for
 sharded / chunked calls), ``forward_u8()`` taking raw uint8 NHWC face crops
-with the normalisation fused into conv1, and ``dtype`` ("bf16" or "fp16": the
-16-bit MFMA operand type; accumulation is fp32 either way).
+with the normalisation fused into conv1, and ``dtype`` ("fp16" or "bf16": the
+16-bit MFMA operand type; accumulation is fp32 either way).  The default is
+"fp16", the parity-grade mode (per-frame probabilities within the north
+star's 1e-3 of the fp32 reference, DESIGN.md §3.5) at the same MFMA rate;
+"bf16" -- which bench.py selects for the bf16 throughput metric -- moves
+them by up to ~3e-3 on the synthetic weights and is an explicit opt-in.
 """
 from __future__ import annotations
 
@@ -64,7 +68,7 @@ def _init_tensor(shape, kind):
 
 class CViT(nn.Module):
     def __init__(self, image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
-                 mlp_dim=2048, *, dtype: str = "bf16"):
+                 mlp_dim=2048, *, dtype: str = "fp16"):
         super().__init__()
         assert image_size % patch_size == 0, "image dimensions must be divisible by the patch size"
         cfg = dict(image_size=image_size, patch_size=patch_size, num_classes=num_classes, channels=channels, dim=dim,

@@ -66,7 +66,7 @@ def _init_tensor(name, shape, kind):
 
 class ResVitKan(nn.Module):
     def __init__(self, image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
-                 mlp_dim=2048, *, dtype: str = "bf16"):
+                 mlp_dim=2048, *, dtype: str = "fp16"):
         super().__init__()
         cfg = dict(image_size=image_size, patch_size=patch_size, num_classes=num_classes, channels=channels, dim=dim,
                    depth=depth, heads=heads, mlp_dim=mlp_dim)

@@ -48,7 +48,7 @@ def _init_tensor(shape, kind):
 
 
 class S3D(nn.Module):
-    def __init__(self, num_class: int, SRM_net: str, *, dtype: str = "bf16"):
+    def __init__(self, num_class: int, SRM_net: str, *, dtype: str = "fp16"):
         super().__init__()
         if dtype not in _lib.DTYPES:
             raise ValueError(f"dtype must be one of {list(_lib.DTYPES)}")

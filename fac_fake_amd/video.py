@@ -54,13 +54,14 @@ def synthetic_video(n_frames: int, height: int = 1080, width: int = 1920, seed: 
                     faces_per_frame: int = 1):
     """Deterministic synthetic video: uint8 BGR frames [F, H, W, 3] on `device`
     (torch's seeded device generator) and face boxes int32 [F*k, 5] =
-    (frame, left, top, right, bottom), square boxes of 240..559 px inside the
-    frame (splitmix64 of `seed`)."""
+    (frame, left, top, right, bottom), square boxes of 112..559 px inside the
+    frame (splitmix64 of `seed`) -- about a quarter of them under 224 px, so
+    both of cv2's INTER_AREA branches (area average / upscale) are exercised."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device=dev).manual_seed(seed)
     frames = torch.randint(0, 256, (n_frames, height, width, 3), dtype=torch.uint8, device=dev, generator=g)
     r = splitmix64(np.arange(3 * n_frames * faces_per_frame, dtype=np.uint64), seed + 1000).reshape(-1, 3)
-    size = 240 + (r[:, 0] % np.uint64(320)).astype(np.int64)
+    size = 112 + (r[:, 0] % np.uint64(448)).astype(np.int64)
     size = np.minimum(size, min(height, width))
     left = (r[:, 1] % (np.uint64(width) - size.astype(np.uint64) + np.uint64(1))).astype(np.int64)
     top = (r[:, 2] % (np.uint64(height) - size.astype(np.uint64) + np.uint64(1))).astype(np.int64)

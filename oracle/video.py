@@ -18,6 +18,22 @@ TEST INFRASTRUCTURE ONLY (the checker, never the product path).
   The HIP kernel (fac_fake_amd/csrc/crop.hip) evaluates the same integers.
   cv2 is absent from the image, so agreement with cv2 itself (float weights,
   possible 1-count differences on exact .5 ties) is unpinned.
+* cv2 computes true area averages only when BOTH axes shrink or keep their
+  size (a box of at least 224 px on each side).  Otherwise -- a face box under
+  224 px on either axis, common on 480p/720p footage -- ``cv2.resize`` runs
+  its bilinear path with area-mode coefficients on both axes
+  (``linear_area_coeffs``: source index floor(d*scale), fraction
+  (d+1) - (s+1)/scale wrapped to [0,1), 11-bit fixed-point taps), a
+  horizontal pass in exact integers and the vertical pass of its SIMD kernel
+  for uint8 (``VResizeLinearVec_32s8u``: rows >> 4, 16-bit mulhi with the row
+  taps, (sum + 2) >> 2, saturate).  ``crop_resize_area`` takes that branch
+  whenever the clipped box is under 224 px on either axis.  This restates
+  OpenCV's published algorithm (opencv/modules/imgproc/src/resize.cpp,
+  ``hal::resize`` / ``resizeGeneric_`` / ``HResizeLinear`` /
+  ``VResizeLinearVec_32s8u``, OpenCV 4.x, 128/256-bit SIMD builds); the
+  reference pins no OpenCV version and cv2 is not in the image, so parity
+  with cv2 on these boxes is unpinned (non-SIMD builds round the vertical
+  pass as (b0 D0 + b1 D1 + 2^21) >> 22 and can differ by one count).
 """
 from __future__ import annotations
 
@@ -48,6 +64,47 @@ def overlap_matrix(n: int) -> np.ndarray:
     return np.maximum(hi - lo, 0)
 
 
+def linear_area_coeffs(n: int, clamp_fraction: bool):
+    """cv2's INTER_AREA coefficients on a non-downscale (hal::resize's
+    ``area_mode`` branch of the x and y coefficient loops), n source pixels ->
+    224: per output pixel d, the first source index s and the fixed-point
+    taps (a0, a1) of s and s + 1 in units of 1/2048.  ``clamp_fraction``: the
+    x loop also pins s = n - 1 with fraction 0 once s + 1 leaves the span
+    (the y loop leaves the fraction alone and clips the row indices)."""
+    inv = CROP / n           # inv_scale = (double)dsize / ssize
+    scale = 1.0 / inv        # scale = 1. / inv_scale
+    s_out = np.empty(CROP, np.int64)
+    taps = np.empty((CROP, 2), np.int64)
+    for d in range(CROP):
+        s = int(np.floor(d * scale))
+        f = np.float32((d + 1) - (s + 1) * inv)            # (float)((d+1) - (s+1)*inv_scale), double math
+        f = np.float32(0.0) if f <= 0 else np.float32(f - np.float32(np.floor(f)))
+        if clamp_fraction and s >= n - 1:
+            s, f = n - 1, np.float32(0.0)
+        s_out[d] = s
+        c0, c1 = np.float32(np.float32(1.0) - f), f
+        taps[d] = (int(np.rint(np.float32(c0 * np.float32(2048)))),
+                   int(np.rint(np.float32(c1 * np.float32(2048)))))  # saturate_cast<short>: round half even
+    return s_out, taps
+
+
+def _resize_linear_area(src: np.ndarray) -> np.ndarray:
+    """src int64 [ny, nx, 3] (box, BGR) -> uint8 [224, 224, 3] BGR, cv2's
+    bilinear-with-area-coefficients path (see the module docstring)."""
+    ny, nx = src.shape[:2]
+    sx, ax = linear_area_coeffs(nx, True)
+    sy, by = linear_area_coeffs(ny, False)
+    sx1 = np.minimum(sx + 1, nx - 1)   # a1 == 0 wherever the second tap is clamped
+    # horizontal pass, exact integers: D[row, d, c] = S[row, sx] a0 + S[row, sx+1] a1
+    D = src[:, sx, :] * ax[None, :, 0, None] + src[:, sx1, :] * ax[None, :, 1, None]
+    r0 = np.clip(sy, 0, ny - 1)
+    r1 = np.clip(sy + 1, 0, ny - 1)
+    h0 = np.minimum(D[r0] >> 4, 32767)            # v_pack(v_shr<4>(S)) (saturating to int16)
+    h1 = np.minimum(D[r1] >> 4, 32767)
+    v = ((h0 * by[:, 0, None, None]) >> 16) + ((h1 * by[:, 1, None, None]) >> 16)   # v_mul_hi
+    return np.clip((v + 2) >> 2, 0, 255).astype(np.uint8)                          # v_rshr_pack_u<2>
+
+
 def crop_resize_area(frame: np.ndarray, box) -> np.ndarray:
     """frame: uint8 [H, W, 3] BGR; box = (left, top, right, bottom) -> uint8 [224, 224, 3] RGB."""
     H, W = frame.shape[:2]
@@ -56,6 +113,8 @@ def crop_resize_area(frame: np.ndarray, box) -> np.ndarray:
     if x1 <= x0 or y1 <= y0:
         return np.zeros((CROP, CROP, 3), np.uint8)
     src = frame[y0:y1, x0:x1].astype(np.int64)
+    if (x1 - x0) < CROP or (y1 - y0) < CROP:
+        return np.ascontiguousarray(_resize_linear_area(src)[:, :, ::-1])  # BGR -> RGB
     ry, rx = overlap_matrix(y1 - y0), overlap_matrix(x1 - x0)
     den = (x1 - x0) * (y1 - y0)
     out = np.empty((CROP, CROP, 3), np.uint8)

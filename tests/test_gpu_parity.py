@@ -428,17 +428,22 @@ def test_pipelined_forward_matches_synchronous(models):
 
 
 def test_crop_resize_kernel_matches_oracle():
-    """fac_crop_resize_u8 (crop + INTER_AREA area weights in exact integers +
-    BGR->RGB) is bit-identical to oracle/video.py on downscales (odd and
-    even sizes), the 224 identity, upscales, boxes clipped by the frame,
-    empty boxes and out-of-range frame indices."""
+    """fac_crop_resize_u8 (crop + INTER_AREA + BGR->RGB) is bit-identical to
+    oracle/video.py on downscales (odd and even sizes; exact-integer area
+    weights), the 224 identity, boxes under 224 px on one or both axes (cv2's
+    bilinear-with-area-coefficients branch: enlargements, mixed
+    shrink/enlarge, integer factors, 1-px and 223-px boxes), boxes clipped by
+    the frame, empty boxes and out-of-range frame indices."""
     from fac_fake_amd.video import crop_faces
     from oracle import video as ov
     rng = np.random.default_rng(11)
     frames = rng.integers(0, 256, (5, 720, 1280, 3), dtype=np.uint8)
     boxes = np.array([[0, 10, 20, 234, 244], [1, 100, 50, 551, 501], [2, 0, 0, 333, 257], [3, 1000, 400, 1280, 720],
                       [4, 37, 41, 137, 141], [0, 1200, 600, 1500, 900], [1, -30, -40, 270, 260],
-                      [2, 5, 5, 5, 300], [9, 0, 0, 300, 300], [4, 640, 0, 641, 720], [3, 3, 7, 1279, 719]],
+                      [2, 5, 5, 5, 300], [9, 0, 0, 300, 300], [4, 640, 0, 641, 720], [3, 3, 7, 1279, 719],
+                      [0, 0, 0, 300, 150], [1, 50, 60, 200, 500], [2, 10, 10, 122, 122], [3, 7, 9, 8, 10],
+                      [4, 100, 100, 323, 323], [0, 500, 300, 724, 524], [1, 0, 0, 224, 223], [2, 17, 3, 49, 35],
+                      [3, 900, 100, 1077, 290]],
                      np.int32)
     got = crop_faces(torch.from_numpy(frames).to(DEV), boxes).cpu().numpy()
     want = ov.crop_batch(frames, boxes)

@@ -74,7 +74,81 @@ def test_synthetic_video_is_deterministic_and_in_frame():
     f2, b2 = video.synthetic_video(4, 300, 500, seed=5, device="cpu")
     assert torch.equal(f1, f2) and np.array_equal(b1, b2)
     assert (b1[:, 1] >= 0).all() and (b1[:, 3] <= 500).all() and (b1[:, 2] >= 0).all() and (b1[:, 4] <= 300).all()
-    assert ((b1[:, 3] - b1[:, 1]) >= 240).all()
+    assert ((b1[:, 3] - b1[:, 1]) >= 112).all()
+    _, b3 = video.synthetic_video(1, 1080, 1920, seed=3, device="cpu", faces_per_frame=64)
+    side = b3[:, 3] - b3[:, 1]
+    assert (side < 224).any() and (side >= 224).any()   # both INTER_AREA branches occur
+
+
+def _linear_area_scalar(frame, box):
+    """Independent scalar loop over cv2's bilinear-with-area-coefficients
+    resize for uint8 (resize.cpp: coefficient loops of hal::resize,
+    HResizeLinear, VResizeLinearVec_32s8u), used to check the vectorised
+    restatement in oracle/video.py."""
+    import math
+    x0, y0, x1, y1 = box
+    src = frame[y0:y1, x0:x1].astype(np.int64)
+    ny, nx = src.shape[:2]
+
+    def coeffs(n, d, clamp):
+        inv = 224 / n
+        scale = 1.0 / inv
+        s = math.floor(d * scale)
+        f = np.float32((d + 1) - (s + 1) * inv)
+        f = np.float32(0) if f <= 0 else np.float32(f - np.float32(math.floor(f)))
+        if clamp and s >= n - 1:
+            s, f = n - 1, np.float32(0)
+        a0 = int(np.rint(np.float32((np.float32(1) - f) * np.float32(2048))))
+        a1 = int(np.rint(np.float32(f * np.float32(2048))))
+        return s, a0, a1
+
+    out = np.zeros((224, 224, 3), np.uint8)
+    for dy in range(224):
+        sy, b0, b1 = coeffs(ny, dy, False)
+        rows = (min(sy, ny - 1), min(sy + 1, ny - 1))
+        for dx in range(224):
+            sx, a0, a1 = coeffs(nx, dx, True)
+            for c in range(3):
+                h = [min((src[r, sx, c] * a0 + src[r, min(sx + 1, nx - 1), c] * a1) >> 4, 32767) for r in rows]
+                v = ((h[0] * b0) >> 16) + ((h[1] * b1) >> 16)
+                out[dy, dx, 2 - c] = min(max((v + 2) >> 2, 0), 255)
+    return out
+
+
+@pytest.mark.parametrize("k", [2, 4, 8])   # power-of-two factors: scale and 1/scale are exact doubles
+def test_area_resize_integer_upscale_replicates_pixels(k):
+    """cv2 INTER_AREA enlarging by an integer factor: the area-mode
+    fractions are all 0, so every source pixel is repeated k x k times."""
+    n = 224 // k
+    rng = np.random.default_rng(k)
+    frame = rng.integers(0, 256, (n + 10, n + 12, 3), dtype=np.uint8)
+    out = ov.crop_resize_area(frame, (3, 5, 3 + n, 5 + n))
+    exp = np.repeat(np.repeat(frame[5:5 + n, 3:3 + n], k, 0), k, 1)[:, :, ::-1]
+    assert np.array_equal(out, exp)
+
+
+@pytest.mark.parametrize("box", [(3, 4, 103, 104),      # 100 x 100: both axes enlarge
+                                 (0, 0, 300, 150),      # x shrinks, y enlarges (mixed)
+                                 (10, 2, 160, 402),     # x enlarges, y shrinks (mixed)
+                                 (5, 7, 228, 230),      # 223 x 223
+                                 (1, 1, 2, 2),          # one pixel
+                                 (0, 0, 224, 131)])     # x identity, y enlarges
+def test_linear_area_branch_matches_scalar_restatement(box):
+    rng = np.random.default_rng(sum(box))
+    frame = rng.integers(0, 256, (420, 320, 3), dtype=np.uint8)
+    got = ov.crop_resize_area(frame, box)
+    assert np.array_equal(got, _linear_area_scalar(frame, box))
+
+
+def test_linear_area_branch_constant_and_identity_axis():
+    frame = np.full((200, 300, 3), 200, np.uint8)
+    frame[..., 1] = 7
+    out = ov.crop_resize_area(frame, (0, 0, 150, 90))
+    assert (np.abs(out.astype(int) - frame[0, 0, ::-1].astype(int)) <= 1).all()
+    rng = np.random.default_rng(1)
+    frame = rng.integers(0, 256, (120, 224, 3), dtype=np.uint8)
+    out = ov.crop_resize_area(frame, (0, 0, 224, 112))   # x keeps its size, y doubles
+    assert np.array_equal(out, np.repeat(frame[:112], 2, 0)[:, :, ::-1])
 
 
 class _StandInModel:
