@@ -186,6 +186,13 @@ class ResVitKan(nn.Module):
     # just fill the 256 CUs worse (tools/rvk_chunks.sh)
     feature_chunk = 0
 
+    def _side_stream(self, device: torch.device):
+        st = getattr(self, "_side", None)
+        if st is None or st.device != device:
+            st = torch.cuda.Stream(device)
+            self._side = st
+        return st
+
     def features16(self, x16: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """ResNet.forward (ResVitKan.py:232-247) on space-to-depth packed 16-bit
         cells [B,1,115,115,16] (ops.pack_input_s2d) -> [B,1,7,7,512] 16-bit
@@ -198,8 +205,19 @@ class ResVitKan(nn.Module):
             x = self._conv1(x16[b0:b0 + step])                      # 7x7/2 + bn1 + ReLU, on s2d cells
             x = pool(x, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")     # MaxPool2d(3, 2, 1)
             for c1, c2, c3, ds in self._blocks:
-                res = ds(x, relu=False) if ds is not None else x
-                h = c2(c1(x))
+                if ds is not None:
+                    # the downsample branch (first block of each layer) runs on a
+                    # side stream beside conv1 -> conv2, joined before conv3 adds it
+                    main = torch.cuda.current_stream(x.device)
+                    side = self._side_stream(x.device)
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        res = ds(x, relu=False)
+                    h = c2(c1(x))
+                    main.wait_stream(side)
+                else:
+                    res = x
+                    h = c2(c1(x))
                 x = c3(h, residual=res, relu2=True)                 # relu(bn3) + residual, relu
             self._channel(x, relu=False, out=out[b0:b0 + step])     # channel 1x1 + bn2
         return out

@@ -136,19 +136,43 @@ class S3D(nn.Module):
         self._prep = (idx, v)
 
     # ------------------------------------------------------------------ forward
-    @staticmethod
-    def _mixed(x, blk):
+    def _branch_streams(self, device: torch.device):
+        """Three side streams (per device) for the Inception branches."""
+        streams = getattr(self, "_side", None)
+        if streams is None or streams[0].device != device:
+            streams = [torch.cuda.Stream(device) for _ in range(3)]
+            self._side = streams
+        return streams
+
+    def _mixed(self, x, blk):
+        """One Mixed_* block (model.py:84-342).  Its four branches read the same
+        input and write disjoint channel slots of the block output, so they
+        run concurrently: branch 0 on the current stream, branches 1-3 on side
+        streams forked from it and joined back before the output is used (a
+        hipGraph capture turns this into four parallel chains of nodes).  The
+        late blocks' launches are latency-bound (4x7 and 2x3 maps: 100-200
+        workgroups each), so overlapping the chains shortens the block instead
+        of leaving most CUs idle between dependent launches."""
         n, d, h, w, _ = x.shape
         out = torch.empty(n, d, h, w, sum(blk["widths"]), dtype=x.dtype, device=x.device)
         o1 = blk["widths"][0]
         o2 = o1 + blk["widths"][1]
         o3 = o2 + blk["widths"][2]
+        main = torch.cuda.current_stream(x.device)
+        side = self._branch_streams(x.device)
+        for s in side:
+            s.wait_stream(main)
+        with torch.cuda.stream(side[0]):
+            s1, t1 = blk["b1"]
+            t1(s1(blk["b1a"](x)), out=out, c_off=o1)
+        with torch.cuda.stream(side[1]):
+            s2, t2 = blk["b2"]
+            t2(s2(blk["b2a"](x)), out=out, c_off=o2)
+        with torch.cuda.stream(side[2]):
+            blk["b3"](pool(x, 3, 1, 1, "max"), out=out, c_off=o3)    # MaxPool3d(3, 1, 1) then 1x1x1
         blk["b0"](x, out=out, c_off=0)
-        s1, t1 = blk["b1"]
-        t1(s1(blk["b1a"](x)), out=out, c_off=o1)
-        s2, t2 = blk["b2"]
-        t2(s2(blk["b2a"](x)), out=out, c_off=o2)
-        blk["b3"](pool(x, 3, 1, 1, "max"), out=out, c_off=o3)        # MaxPool3d(3, 1, 1) then 1x1x1
+        for s in side:
+            main.wait_stream(s)
         return out
 
     def features16(self, x16: torch.Tensor) -> torch.Tensor:
