@@ -116,6 +116,50 @@ def video_measurement(model, dev, world: int, n_frames: int = 300, reps: int = 3
 
 
 RESVITKAN_FLOP_PER_CROP = 8.53e9   # conv + linear MACs x 2 of ResVitKan.py (KAN excluded)
+HBM_PEAK_TBS = 8.0                 # MI355X HBM3E (MI355X_MICROARCH.md; ~6.3 TB/s achievable)
+
+
+def layer_roofline_ms(run, dtype: str) -> dict:
+    """Per-layer roofline of the fac_conv_nd / fac_pool_nd layers one eager
+    `run()` launches: each layer bounded by max(algorithmic FLOPs / dense
+    MFMA peak, minimum HBM bytes (input read once, output (+ residual)
+    written / read once) / HBM peak), summed.  The ResNet-50 and S3D layers
+    at these batch sizes are mostly HBM-bound (arithmetic intensity under the
+    ~312 FLOP/B ridge), so the MFMA-only fraction understates them."""
+    from fac_fake_amd import ops, resvitkan, s3d
+    recs = []
+    orig_call, orig_pool = ops.ConvLayer.__call__, ops.pool
+
+    def conv_hook(self, x, **kw):
+        out = orig_call(self, x, **kw)
+        n, d, h, w, c = x.shape
+        od, oh, ow = self.out_dims(d, h, w)
+        M = n * od * oh * ow
+        flops = 2.0 * M * self.cout * self.g.kd * self.g.kh * self.g.kw * self.cin
+        esz = 4 if kw.get("out_f32") else 2
+        byts = 2.0 * x.numel() + esz * M * self.cout + (2.0 * M * self.cout if kw.get("residual") is not None else 0)
+        recs.append((flops, byts))
+        return out
+
+    def pool_hook(x, *a, **kw):
+        out = orig_pool(x, *a, **kw)
+        recs.append((0.0, 2.0 * (x.numel() + out.numel())))
+        return out
+
+    ops.ConvLayer.__call__ = conv_hook
+    resvitkan.pool = s3d.pool = pool_hook
+    try:
+        run()
+        torch.cuda.synchronize()
+    finally:
+        ops.ConvLayer.__call__ = orig_call
+        resvitkan.pool = s3d.pool = orig_pool
+    peak = PEAK_TFLOPS[dtype] * 1e12
+    t_mfma = sum(f for f, _ in recs) / peak
+    t_hbm = sum(b for _, b in recs) / (HBM_PEAK_TBS * 1e12)
+    t_roof = sum(max(f / peak, b / (HBM_PEAK_TBS * 1e12)) for f, b in recs)
+    return {"layers": len(recs), "roofline_ms": round(t_roof * 1e3, 4), "mfma_only_ms": round(t_mfma * 1e3, 4),
+            "hbm_only_ms": round(t_hbm * 1e3, 4)}
 
 
 def resvitkan_measurement(dev, dtype: str, world: int, B: int = 256, steps: int = 10, warmup: int = 3,
@@ -158,11 +202,16 @@ def resvitkan_measurement(dev, dtype: str, world: int, B: int = 256, steps: int 
     v = world * B * steps / el
     peak = PEAK_TFLOPS[dtype]
     assert torch.isfinite(out).all()
+    with torch.cuda.stream(s):
+        lr = layer_roofline_ms(lambda: m.forward_u8(crops, pos_index=pidx), dtype)
+    ms = el / steps * 1e3
+    lr["fraction_of_step"] = round(lr["roofline_ms"] / ms, 4)
     return {"workload": f"config 5: ResVitKan forward (ResNet-50 + CViT encoder + KAN head), B={B} crops per GPU, "
                         "hipGraph per step", "value": round(v, 1), "unit": "face-crops/s", "n_gpus": world,
-            "ms_per_step": round(el / steps * 1e3, 3), "dtype": dtype,
+            "ms_per_step": round(ms, 3), "dtype": dtype,
             "feature_chunk": m.feature_chunk,
-            "mfma_roofline_fraction": round(v * RESVITKAN_FLOP_PER_CROP / (world * peak * 1e12), 4)}
+            "mfma_roofline_fraction": round(v * RESVITKAN_FLOP_PER_CROP / (world * peak * 1e12), 4),
+            "conv_pool_layer_roofline": lr}
 
 
 S3D_FLOP_PER_CLIP = 8.95e9   # per 16x112x112 clip (Conv3d hooks over S3D/model.py)
@@ -201,10 +250,15 @@ def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, w
         el = float(t.item())
     v = world * B * steps / el
     assert torch.isfinite(out).all()
+    with torch.cuda.stream(s):
+        lr = layer_roofline_ms(lambda: m(x), dtype)
+    ms = el / steps * 1e3
+    lr["fraction_of_step"] = round(lr["roofline_ms"] / ms, 4)
     return {"workload": f"config 4: S3D forward (SRM_net={srm}), B={B} raw 16x112x112 clips per GPU, hipGraph per step",
-            "value": round(v, 1), "unit": "clips/s", "n_gpus": world, "ms_per_step": round(el / steps * 1e3, 3),
+            "value": round(v, 1), "unit": "clips/s", "n_gpus": world, "ms_per_step": round(ms, 3),
             "dtype": dtype,
-            "mfma_roofline_fraction": round(v * S3D_FLOP_PER_CLIP / (world * PEAK_TFLOPS[dtype] * 1e12), 4)}
+            "mfma_roofline_fraction": round(v * S3D_FLOP_PER_CLIP / (world * PEAK_TFLOPS[dtype] * 1e12), 4),
+            "conv_pool_layer_roofline": lr}
 
 
 REPBN8_FLOP_PER_CROP = 13.2915e9 + 2 * 56 * 56 * 128 * 128 * 9   # CViT + the extra 128->128 conv at 56^2
