@@ -22,6 +22,8 @@
 // epilogue stages the fp32 tile in LDS and writes 16-byte channel vectors
 // (bias, ReLU, residual, ReLU, convert), so a row's BN channels leave in one
 // contiguous burst.
+#include <algorithm>
+
 #include "common.hpp"
 #include "fac_cvit.h"
 #include "fac_ops.h"
@@ -528,6 +530,101 @@ __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, fl
   if (t < n) y[t] = 1.f / (1.f + expf(-x[t]));
 }
 
+
+// ---- conv_s2d4: the 4x4 / stride-1 conv over 16-channel space-to-depth cells
+// that the 7x7/2 first convs become (fac_pack_input_s2d): ResNet-50's conv1
+// (ResVitKan.py:187, 3 -> 64) and S3D's (1,7,7)/(1,2,2) spatial half of
+// base.0 (model.py:18), both + folded BN + ReLU, cout 64.  Through the
+// generic implicit GEMM this layer is its costliest (K = 256 in 4 short
+// k-steps per 128-row tile, every tile re-reading the 32 KB weight and
+// paying a prologue and an LDS-staged epilogue).  Here a workgroup keeps the
+// whole weight in LDS and walks output boxes of 8 x 28 positions: per box
+// the (11 x 31)-cell halo (2 x 16-byte channel pieces per cell) is copied to
+// LDS once and all 16 taps read it.  MFMAs run transposed (C^T = W . X^T:
+// rows = channels), so each lane ends with 4 consecutive channels of one
+// position and the epilogue stores 8 bytes straight from registers.
+// k-step s covers taps 2s, 2s+1 (ty = s/2, tx = 2(s%2) + g/2) x 16 channels:
+// lane group g reads channel piece g%2 of tap 2s + g/2, i.e. k = 32s + 8g + e,
+// the natural fac_conv_nd weight order.
+template <class T>
+__global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                    const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                    int nbox, int Hc, int Wc, int Ho, int Wo, int kp, int relu_on) {
+  constexpr int TH = 8, TW = 28, HH = TH + 3, HWD = TW + 3, RPX = 32;  // halo rows, cols, row pitch (cells)
+  constexpr int HSL = 2 * HH * RPX;                                       // 16-byte halo slots
+  constexpr int HPW = (HSL + 255) / 256;                                  // glds per wave
+  constexpr int WEL = 64 * 256;                                           // weight elements
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + HPW * 256 * 8];
+  uint16_t* const sw = smem;
+  uint16_t* const halo = smem + WEL;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // weights [s][ct][g][r16][8]: the A fragment of (k-step s, channel tile ct)
+  // is one contiguous, conflict-free 1 KB read
+  for (int c = tid; c < 64 * 32; c += 256) {
+    const int n = c >> 5, k8 = c & 31;
+    *(u16x8*)(sw + ((((k8 >> 2) * 4 + (n >> 4)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+        *(const u16x8*)(w + (size_t)n * kp + k8 * 8);
+  }
+  float bv[2][4];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias[(2 * wn + ct) * 16 + 4 * g + j];
+  // this lane's halo slot offsets (16-byte units) for pixel tile i at tap (0, g/2)
+  int bo[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int m = (wm * 7 + i) * 16 + r16, py = m / TW, px = m - (m / TW) * TW;
+    bo[i] = ((g & 1) * HH + py) * RPX + px + (g >> 1);
+  }
+  const int bpr = Wo / TW, bpi = (Ho / TH) * bpr;
+  for (int bx = blockIdx.x; bx < nbox; bx += gridDim.x) {
+    const int img = bx / bpi, rr = bx - img * bpi;
+    const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
+    __syncthreads();  // the previous box's halo reads are done (and, first time, the weights are in)
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int sl = (i * 4 + wave) * 64 + lane;
+      const int pc = sl / (HH * RPX), rem = sl - pc * (HH * RPX), hy = rem / RPX, hx = rem - (rem / RPX) * RPX;
+      const uint16_t* src = g_zero16;
+      if (pc < 2 && hx < HWD) src = in + (((size_t)img * Hc + y0 + hy) * Wc + x0 + hx) * 16 + pc * 8;
+      glds16(src, halo + (i * 4 + wave) * 64 * 8);
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    f32x4 acc[7][2];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) acc[i][0] = acc[i][1] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u16x8 wf[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw + (((s * 4 + 2 * wn + ct) * 4 + g) * 16 + r16) * 8);
+      const int so = (s >> 1) * RPX + (s & 1) * 2;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const u16x8 pf = *(const u16x8*)(halo + (bo[i] + so) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(wf[ct], pf, acc[i][ct]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int m = (wm * 7 + i) * 16 + r16, py = m / TW, px = m - (m / TW) * TW;
+      uint16_t* o = out + (((size_t)img * Ho + y0 + py) * Wo + x0 + px) * 64 + 4 * g;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = relu_on ? relu(acc[i][ct][j] + bv[ct][j]) : acc[i][ct][j] + bv[ct][j];
+        *(u16x4*)(o + (2 * wn + ct) * 16) = T::pack4(v);
+      }
+    }
+  }
+}
+
 template <class T>
 static hipError_t launch_convnd(const ConvP& p, int cout_pad, hipStream_t st) {
   (void)cout_pad;
@@ -616,6 +713,25 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   p.vec_res = (d->ldr % 8 == 0 && d->r_off % 8 == 0) ? 1 : 0;
   p.M = (int)M;
   hipStream_t st = (hipStream_t)stream;
+  // the space-to-depth first conv (4x4/1 over 16-channel cells, cout 64, no
+  // residual, dense output): its own kernel (conv_s2d4)
+  if (d->kd == 1 && d->kh == 4 && d->kw == 4 && d->sd == 1 && d->sh == 1 && d->sw == 1 && d->pd == 0 && d->ph == 0 &&
+      d->pw == 0 && d->cin == 16 && d->cout == 64 && k_pad == 256 && d->oh % 8 == 0 && d->ow % 28 == 0 &&
+      d->ldo == 64 && d->c_off == 0 && (d->flags & ~FAC_CONV_RELU) == 0) {
+    const int nimg = d->n * d->od, nbox = nimg * (d->oh / 8) * (d->ow / 28);
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+    const int grid = std::min(nbox, 3 * ncu);
+    const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
+    if (d->dtype == FAC_DTYPE_BF16)
+      conv_s2d4<BF16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
+                                            (uint16_t*)d->out, nbox, d->h, d->w, d->oh, d->ow, k_pad, relu_on);
+    else
+      conv_s2d4<F16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
+                                           (uint16_t*)d->out, nbox, d->h, d->w, d->oh, d->ow, k_pad, relu_on);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
   const hipError_t e = d->dtype == FAC_DTYPE_BF16 ? launch_convnd<BF16>(p, cout_pad, st) : launch_convnd<F16>(p, cout_pad, st);
   return e == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
