@@ -128,7 +128,8 @@ def layer_roofline_ms(run, dtype: str) -> dict:
     ~312 FLOP/B ridge), so the MFMA-only fraction understates them."""
     from fac_fake_amd import ops, resvitkan, s3d
     recs = []
-    orig_call, orig_pool = ops.ConvLayer.__call__, ops.pool
+    orig_call, orig_pool, orig_sep = ops.ConvLayer.__call__, ops.pool, ops.max_pool_sep
+    in_sep = [False]
 
     def conv_hook(self, x, **kw):
         out = orig_call(self, x, **kw)
@@ -143,17 +144,29 @@ def layer_roofline_ms(run, dtype: str) -> dict:
 
     def pool_hook(x, *a, **kw):
         out = orig_pool(x, *a, **kw)
+        if not in_sep[0]:
+            recs.append((0.0, 2.0 * (x.numel() + out.numel())))
+        return out
+
+    def sep_hook(x, *a, **kw):   # one pooling layer (its per-axis passes are an implementation detail)
+        in_sep[0] = True
+        try:
+            out = orig_sep(x, *a, **kw)
+        finally:
+            in_sep[0] = False
         recs.append((0.0, 2.0 * (x.numel() + out.numel())))
         return out
 
     ops.ConvLayer.__call__ = conv_hook
-    resvitkan.pool = s3d.pool = pool_hook
+    ops.pool = resvitkan.pool = s3d.pool = pool_hook
+    resvitkan.max_pool_sep = s3d.max_pool_sep = sep_hook
     try:
         run()
         torch.cuda.synchronize()
     finally:
         ops.ConvLayer.__call__ = orig_call
-        resvitkan.pool = s3d.pool = orig_pool
+        ops.pool = resvitkan.pool = s3d.pool = orig_pool
+        resvitkan.max_pool_sep = s3d.max_pool_sep = orig_sep
     peak = PEAK_TFLOPS[dtype] * 1e12
     t_mfma = sum(f for f, _ in recs) / peak
     t_hbm = sum(b for _, b in recs) / (HBM_PEAK_TBS * 1e12)

@@ -181,6 +181,24 @@ def pool(x: torch.Tensor, kernel, stride, padding=0, mode: str = "max", out: tor
     return out
 
 
+def max_pool_sep(x: torch.Tensor, kernel, stride, padding=0) -> torch.Tensor:
+    """Max pooling as one fac_pool_nd pass per axis (W, then H, then D; axes
+    with kernel 1, stride 1 and no padding are skipped).  A max over a box
+    window (padding ignored, i.e. -inf) is the max over its rows of the max
+    over its columns, so the result is bit-identical to one 3-D pass, while
+    each output reads kw + kh + kd inputs instead of kw * kh * kd (27 -> 9
+    for S3D's 3x3x3 pools) and the strided axes shrink the later passes."""
+    k, s, p = _triple(kernel), _triple(stride), _pads(padding)
+    y = x
+    for ax in (2, 1, 0):
+        if k[ax] == 1 and s[ax] == 1 and p[ax] == 0:
+            continue
+        kk, ss, pp = [1, 1, 1], [1, 1, 1], [0, 0, 0]
+        kk[ax], ss[ax], pp[ax] = k[ax], s[ax], p[ax]
+        y = pool(y, tuple(kk), tuple(ss), tuple(pp), "max")
+    return y if y is not x else pool(x, kernel, stride, padding, "max")
+
+
 def pack_input(src: torch.Tensor, *, dtype: str, u8: bool, div: float = 1.0, mean=None, std=None,
                spatial: tuple[int, ...]) -> torch.Tensor:
     """3-channel images -> 16-bit [N, D, H, W, 8] (fac_pack_input).

@@ -34,7 +34,7 @@ from torch import nn
 
 from . import _lib
 from .cvit import MAX_SLOTS, _Node
-from .ops import TORCH16, ConvLayer, KANLinearLayer, fold_bn, pack_input_s2d, pool, s2d_weight, sigmoid
+from .ops import TORCH16, ConvLayer, KANLinearLayer, fold_bn, max_pool_sep, pack_input_s2d, pool, s2d_weight, sigmoid
 from .weights import kan_grid, resnet50_blocks, resvitkan_param_specs
 
 SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
@@ -203,7 +203,7 @@ class ResVitKan(nn.Module):
         step = self.feature_chunk or B
         for b0 in range(0, B, step):
             x = self._conv1(x16[b0:b0 + step])                      # 7x7/2 + bn1 + ReLU, on s2d cells
-            x = pool(x, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")     # MaxPool2d(3, 2, 1)
+            x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))    # MaxPool2d(3, 2, 1)
             for c1, c2, c3, ds in self._blocks:
                 if ds is not None:
                     # the downsample branch (first block of each layer) runs on a

@@ -28,7 +28,7 @@ from torch import nn
 
 from . import _lib
 from .cvit import _Node
-from .ops import TORCH16, ConvLayer, fold_bn, pack_input, pack_input_s2d, pool, s2d_weight, sigmoid
+from .ops import TORCH16, ConvLayer, fold_bn, max_pool_sep, pack_input, pack_input_s2d, pool, s2d_weight, sigmoid
 from .weights import s3d_base, s3d_param_specs
 
 BN_EPS = 1e-3   # BatchNorm3d(eps=1e-3) in BasicConv3d / SepConv3d (model.py:54,67,71)
@@ -169,7 +169,7 @@ class S3D(nn.Module):
             s2, t2 = blk["b2"]
             t2(s2(blk["b2a"](x)), out=out, c_off=o2)
         with torch.cuda.stream(side[2]):
-            blk["b3"](pool(x, 3, 1, 1, "max"), out=out, c_off=o3)    # MaxPool3d(3, 1, 1) then 1x1x1
+            blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)   # MaxPool3d(3, 1, 1) then 1x1x1
         blk["b0"](x, out=out, c_off=0)
         for s in side:
             main.wait_stream(s)
@@ -188,7 +188,7 @@ class S3D(nn.Module):
             elif kind == "basic":
                 y = L(y)
             elif kind == "pool":
-                y = pool(y, *L, mode="max")
+                y = max_pool_sep(y, *L)
             else:
                 y = self._mixed(y, L)
         return y
