@@ -492,12 +492,18 @@ namespace fac {
 //    14: 14x14 box, BN 128, 1x4 waves (208 rows for 196 pixels)
 // (the 224 layers normally run inside stem224.hip; the 16x16/BN 32 kernel
 // serves the unfused debug path)
-int conv_block_n(int H) {
+//
+// Other output widths (the ResNet-50 and S3D 3x3 layers routed here by
+// fac_fake_amd/ops.py): 56: BN 64 (8x28 box, 2x2 waves); 28: BN 192 / 128
+// (4x28 box, 1x4 waves).  0 = shape not supported.
+int conv_block_n(int H, int cout) {
   switch (H) {
-    case 224: return 32;
-    case 112: return 64;
-    case 28: return 256;
-    default: return 128;
+    case 224: return cout == 32 ? 32 : 0;
+    case 112: return cout % 64 == 0 ? 64 : 0;
+    case 56: return cout % 128 == 0 ? 128 : (cout % 64 == 0 ? 64 : 0);
+    case 28: return cout % 256 == 0 ? 256 : (cout % 192 == 0 ? 192 : (cout % 128 == 0 ? 128 : 0));
+    case 14: return cout % 128 == 0 ? 128 : 0;
+    default: return 0;
   }
 }
 
@@ -518,14 +524,17 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
                                 int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st,
                                 int relu) {
   if (W != H) return hipErrorInvalidValue;
-  switch (H) {
-    case 224: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+  switch (H * 1000 + conv_block_n(H, Cout)) {
+    case 224032: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
     // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
-    case 112: launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 56: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 28: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 14: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 112064: launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 56128: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 56064: launch_box<T, 8, 28, 64, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28256: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28192: launch_box<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28128: launch_box<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 14128: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -21,7 +21,7 @@
 #include "common.hpp"
 
 namespace fac {
-int conv_block_n(int H);
+int conv_block_n(int H, int cout);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,

@@ -18,7 +18,7 @@
 
 namespace fac {
 
-int conv_block_n(int H);
+int conv_block_n(int H, int cout);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st,
                           bool relu);
@@ -34,7 +34,7 @@ static inline uint16_t to16(int dtype, float f) {
 // byte-identical to the LDS image conv3x3_bn_relu streams (conv.hip).
 // w: folded fp32 [cout][cin][9].
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out) {
-  const int BN = conv_block_n(H), CK = 32, nch = ci / CK;
+  const int BN = conv_block_n(H, co), CK = 32, nch = ci / CK;
   size_t q = 0;
   for (int nb = 0; nb < co / BN; ++nb)
     for (int ch = 0; ch < nch; ++ch)
@@ -64,8 +64,8 @@ void pack_stem_conv1(int dtype, const float* w, uint16_t* out) {
 
 static bool conv3x3_shape_ok(int h, int cin, int cout) {
   if (h != 224 && h != 112 && h != 56 && h != 28 && h != 14) return false;
-  if (cin < 32 || cin % 32 || cout <= 0 || cout % conv_block_n(h)) return false;
-  return h != 224 || cout == 32;
+  if (cin < 32 || cin % 32 || cout <= 0) return false;
+  return conv_block_n(h, cout) > 0;
 }
 
 static int num_cus() {

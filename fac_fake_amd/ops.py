@@ -46,6 +46,17 @@ class PoolDesc(ctypes.Structure):
                 ("mode", ctypes.c_int), ("out", ctypes.c_void_p), ("ldo", ctypes.c_int), ("c_off", ctypes.c_int)]
 
 
+_ZERO256: dict = {}
+
+
+def _zero256(device: torch.device) -> torch.Tensor:
+    """256 zero bytes of device memory: the source of conv.hip's zero-padding loads."""
+    key = (device.type, device.index)
+    if key not in _ZERO256:
+        _ZERO256[key] = torch.zeros(128, dtype=torch.int16, device=device)
+    return _ZERO256[key]
+
+
 def _stream(t: torch.Tensor):
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -122,6 +133,32 @@ class ConvLayer:
         b = torch.zeros(self.cout_pad)
         b[:co] = bias.detach().to("cpu", torch.float32)
         self.b = b.to(device)
+        # 3x3 / stride 1 / padding 1 spatial convs with 32-channel chunks (the
+        # ResNet-50 and S3D (1,3,3) layers) run on the CViT conv-stack kernel
+        # (conv.hip: halo staged once per 32-channel chunk for all 9 taps)
+        # wherever it has a tile for the resolution and width: packed per
+        # input size on first use (fac_conv3x3_pack), else fac_conv_nd.
+        self._w33 = None
+        g = self.g
+        if (kd, kh, kw) == (1, 3, 3) and (g.sd, g.sh, g.sw) == (1, 1, 1) and (g.pd, g.ph, g.pw) == (0, 1, 1) \
+                and ci % 32 == 0:
+            self._w33 = w[:, :, 0].reshape(co, ci, 9).contiguous()
+            self._pk33 = {}
+            self._device = device
+
+    def _packed33(self, h: int):
+        """fac_conv3x3 weights for h x h inputs, or None if conv.hip has no tile for it."""
+        if h not in self._pk33:
+            lib = _lib.load()
+            n = lib.fac_conv3x3_packed_elems(h, self.cin, self.cout)
+            pk = None
+            if n:
+                out = torch.empty(n, dtype=torch.int16)
+                _lib.check(lib.fac_conv3x3_pack(_lib.DTYPES[self.dtype], h, self.cin, self.cout, self._w33.data_ptr(),
+                                                out.data_ptr()), None, "fac_conv3x3_pack")
+                pk = out.view(TORCH16[self.dtype]).to(self._device)
+            self._pk33[h] = pk
+        return self._pk33[h]
 
     def out_dims(self, d, h, w):
         g = self.g
@@ -140,6 +177,15 @@ class ConvLayer:
                               dtype=torch.float32 if out_f32 else x.dtype)
         if tuple(out.shape[:4]) != (n, od, oh, ow) or not out.is_contiguous():
             raise ValueError(f"conv output must be contiguous [{n},{od},{oh},{ow},C], got {tuple(out.shape)}")
+        if (self._w33 is not None and h == w and residual is None and not relu2 and not out_f32 and c_off == 0
+                and out.shape[4] == self.cout):
+            pk = self._packed33(h)
+            if pk is not None:
+                lib = _lib.load()
+                _lib.check(lib.fac_conv3x3(_lib.DTYPES[self.dtype], x.data_ptr(), pk.data_ptr(), self.b.data_ptr(),
+                                           out.data_ptr(), n * d, h, self.cin, self.cout, 0, 1 if relu else 0,
+                                           _zero256(x.device).data_ptr(), _stream(x)), None, "fac_conv3x3")
+                return out
         g = self.g
         dsc = ConvDesc()
         dsc.dtype = _lib.DTYPES[self.dtype]

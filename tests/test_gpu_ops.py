@@ -49,6 +49,11 @@ CONV_CASES = [
     (1, 5, 12, 12, 24, 48, (1, 3, 3), 1, (0, 1, 1)),
     (1, 8, 16, 16, 8, 64, (3, 7, 7), 2, (1, 3, 3)),
     (1, 3, 7, 7, 40, 12, (1, 1, 1), 1, 0),
+    # 3x3/1 convs routed to conv.hip's halo kernel (ResNet-50 / S3D widths)
+    (2, 1, 56, 56, 64, 64, (1, 3, 3), 1, (0, 1, 1)),
+    (1, 2, 28, 28, 64, 192, (1, 3, 3), 1, (0, 1, 1)),
+    (2, 1, 28, 28, 128, 128, (1, 3, 3), 1, (0, 1, 1)),
+    (2, 1, 14, 14, 256, 256, (1, 3, 3), 1, (0, 1, 1)),
     # the space-to-depth first conv (ops.hip conv_s2d4: 4x4/1, 16 -> 64, 8 x 28 boxes)
     (2, 2, 19, 31, 16, 64, (1, 4, 4), 1, 0),
     (1, 1, 59, 59, 16, 64, (1, 4, 4), 1, 0),
