@@ -22,6 +22,7 @@ Arithmetic (every layer a HIP kernel of libfac_cvit.so, no CPU fallback):
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import nn
@@ -136,6 +137,14 @@ class S3D(nn.Module):
         self._prep = (idx, v)
 
     # ------------------------------------------------------------------ forward
+    # Opt-in (FAC_S3D_CONCURRENT=1): alone in a process the concurrent
+    # branches measured 21.4k -> 23.3k clips/s (round 2, before the kernel
+    # work below them), but after the CViT bench in the same process the very
+    # same graph ran at 20.5k vs 24.9k serial -- the branch streams come from
+    # torch's stream pool and share the process's 4 hardware queues with
+    # whatever streams exist, so the overlap is not dependable.
+    concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "0") == "1"
+
     def _branch_streams(self, device: torch.device):
         """Three side streams (per device) for the Inception branches."""
         streams = getattr(self, "_side", None)
@@ -159,6 +168,14 @@ class S3D(nn.Module):
         o2 = o1 + blk["widths"][1]
         o3 = o2 + blk["widths"][2]
         main = torch.cuda.current_stream(x.device)
+        if not self.concurrent_branches:
+            s1, t1 = blk["b1"]
+            s2, t2 = blk["b2"]
+            blk["b0"](x, out=out, c_off=0)
+            t1(s1(blk["b1a"](x)), out=out, c_off=o1)
+            t2(s2(blk["b2a"](x)), out=out, c_off=o2)
+            blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
+            return out
         side = self._branch_streams(x.device)
         for s in side:
             s.wait_stream(main)
