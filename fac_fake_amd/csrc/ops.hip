@@ -625,6 +625,104 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
   }
 }
 
+
+// ---- conv_tk: S3D's temporal (kd,1,1) convs with 8 output frames (model.py:
+// 63-82, SepConv3d's conv_t + bn_t + relu_t: base.0's (7,1,1)/(2,1,1) and
+// base.3's (3,1,1) at 56^2 / 28^2 positions).  Through the generic implicit
+// GEMM every output frame re-gathers its kd input frames (3.5 reads of each
+// input element for base.0).  Here a unit is (clip n, 16 consecutive spatial
+// positions): its D x 16 x Cin input slab is copied to LDS once (glds,
+// double-buffered when it fits: the next unit's slab streams in during this
+// one) and wave z computes output frame z for those 16 positions from it,
+// the workgroup's 64-channel weight block resident in LDS
+// ([k-step][ct][g][r16][8], one 1 KB fragment per read).  MFMAs transposed
+// (rows = channels): each lane stores 4 channels of one position straight
+// from registers.  Slab pieces are XOR-swizzled by position (piece j of
+// position p at slot j ^ (p & 7)) so the 16 positions of a fragment read
+// spread over the LDS banks.
+template <class T>
+__global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                  const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                  int nunits, int S, int D, int Cin, int kd, int sd, int pd, int kp,
+                                                  int ldo, int c_off, int relu_on, int db) {
+  constexpr int LDS_EL = 81920;  // 160 KiB
+  __shared__ __attribute__((aligned(16))) uint16_t smem[LDS_EL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int nb = blockIdx.y;
+  const int NP = Cin >> 3, CH = Cin >> 5, KS = kd * CH;  // pieces / 32-channel chunks per position, k-steps
+  const int SLAB = D * 16 * Cin;                          // elements per slab buffer
+  uint16_t* const wts = smem;
+  uint16_t* const slab0 = smem + KS * 2048;
+  const int units_per_clip = S >> 4;
+
+  auto issue_slab = [&](uint16_t* dst, int u) {
+    const int n = u / units_per_clip, p0 = (u - n * units_per_clip) << 4;
+    const int npieces = D * 16 * NP;
+    for (int b = wave * 64; b < npieces; b += 512) {
+      const int sl = b + lane;
+      const int dp = sl / NP, j = sl - dp * NP;     // dp = d * 16 + p
+      const int d = dp >> 4, p = dp & 15;
+      const uint16_t* src = g_zero16;
+      if (d < D) src = in + (((size_t)n * D + d) * S + p0 + p) * Cin + ((j ^ (p & 7)) << 3);
+      glds16(src, dst + b * 8);
+    }
+  };
+
+  int u = blockIdx.x;
+  if (u < nunits) issue_slab(slab0, u);
+  // this workgroup's 64 output channels, all k-steps
+  for (int c = tid; c < 64 * KS * 4; c += 512) {
+    const int n = c / (KS * 4), k8 = c - n * (KS * 4);
+    *(u16x8*)(wts + ((((k8 >> 2) * 4 + (n >> 4)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+        *(const u16x8*)(w + (size_t)(nb * 64 + n) * kp + k8 * 8);
+  }
+  float bv[4][4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias[nb * 64 + ct * 16 + 4 * g + j];
+  const int z = wave;  // output frame of this wave (Do == 8)
+  for (int it = 0; u < nunits; ++it) {
+    const int next = u + gridDim.x;
+    uint16_t* const cur = slab0 + (db == 2 ? (it & 1) * SLAB : 0);
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // slab u in; the other buffer's readers done
+    if (db == 2 && next < nunits) issue_slab(slab0 + ((it + 1) & 1) * SLAB, next);
+    f32x4 acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = (f32x4)0.f;
+    for (int t = 0; t < kd; ++t) {
+      const int d = z * sd + t - pd;
+      if ((unsigned)d >= (unsigned)D) continue;     // zero padding (wave-uniform)
+      const uint16_t* row = cur + (d * 16 + r16) * Cin;
+      const uint16_t* wk = wts + (t * CH * 16 + g) * 128 + r16 * 8;  // [s = t*CH + ch][ct][g][r16][8]
+#pragma unroll 2
+      for (int ch = 0; ch < CH; ++ch) {
+        const u16x8 pf = *(const u16x8*)(row + (((ch * 4 + g) ^ (r16 & 7)) << 3));
+        const uint16_t* wb = wk + ch * 16 * 128;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[ct] = T::mfma(*(const u16x8*)(wb + ct * 4 * 128), pf, acc[ct]);
+      }
+    }
+    {
+      const int n = u / units_per_clip, p0 = (u - n * units_per_clip) << 4;
+      uint16_t* o = out + (((size_t)n * 8 + z) * S + p0 + r16) * ldo + c_off + nb * 64 + 4 * g;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = relu_on ? relu(acc[ct][j] + bv[ct][j]) : acc[ct][j] + bv[ct][j];
+        *(u16x4*)(o + ct * 16) = T::pack4(v);
+      }
+    }
+    if (db == 1) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done with the slab
+      if (next < nunits) issue_slab(slab0, next);
+    }
+    u = next;
+  }
+}
+
 template <class T>
 static hipError_t launch_convnd(const ConvP& p, int cout_pad, hipStream_t st) {
   (void)cout_pad;
@@ -731,6 +829,32 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
       conv_s2d4<F16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
                                            (uint16_t*)d->out, nbox, d->h, d->w, d->oh, d->ow, k_pad, relu_on);
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  // S3D's temporal (kd,1,1) convs with 8 output frames over 16-aligned
+  // spatial maps: conv_tk (LDS slab per 16 positions, weights resident)
+  if (d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 && d->pw == 0 && d->od == 8 &&
+      d->cin % 64 == 0 && d->cout % 64 == 0 && (d->h * d->w) % 16 == 0 && d->ldo % 4 == 0 && d->c_off % 4 == 0 &&
+      (d->flags & ~FAC_CONV_RELU) == 0 && k_pad == d->kd * d->cin) {
+    const int ks = d->kd * d->cin / 32, slab = d->d * 16 * d->cin;
+    const int db = ks * 2048 + 2 * slab <= 81920 ? 2 : (ks * 2048 + slab <= 81920 ? 1 : 0);
+    if (db) {
+      int dev = 0, ncu = 256;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+      const int nunits = d->n * (d->h * d->w / 16);
+      const dim3 grid(std::min(nunits, ncu), d->cout / 64);
+      const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
+      if (d->dtype == FAC_DTYPE_BF16)
+        conv_tk<BF16><<<grid, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
+                                            (uint16_t*)d->out, nunits, d->h * d->w, d->d, d->cin, d->kd, d->sd,
+                                            d->pd, k_pad, d->ldo, d->c_off, relu_on, db);
+      else
+        conv_tk<F16><<<grid, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
+                                           (uint16_t*)d->out, nunits, d->h * d->w, d->d, d->cin, d->kd, d->sd,
+                                           d->pd, k_pad, d->ldo, d->c_off, relu_on, db);
+      return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+    }
   }
   const hipError_t e = d->dtype == FAC_DTYPE_BF16 ? launch_convnd<BF16>(p, cout_pad, st) : launch_convnd<F16>(p, cout_pad, st);
   return e == hipSuccess ? FAC_OK : FAC_ERR_HIP;

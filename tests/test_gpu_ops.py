@@ -54,6 +54,9 @@ CONV_CASES = [
     (1, 2, 28, 28, 64, 192, (1, 3, 3), 1, (0, 1, 1)),
     (2, 1, 28, 28, 128, 128, (1, 3, 3), 1, (0, 1, 1)),
     (2, 1, 14, 14, 256, 256, (1, 3, 3), 1, (0, 1, 1)),
+    # S3D's temporal convs with 8 output frames (ops.hip conv_tk)
+    (2, 16, 8, 8, 64, 64, (7, 1, 1), (2, 1, 1), (3, 0, 0)),
+    (2, 8, 4, 8, 192, 192, (3, 1, 1), 1, (1, 0, 0)),
     # the space-to-depth first conv (ops.hip conv_s2d4: 4x4/1, 16 -> 64, 8 x 28 boxes)
     (2, 2, 19, 31, 16, 64, (1, 4, 4), 1, 0),
     (1, 1, 59, 59, 16, 64, (1, 4, 4), 1, 0),
