@@ -137,19 +137,19 @@ class S3D(nn.Module):
         self._prep = (idx, v)
 
     # ------------------------------------------------------------------ forward
-    # Opt-in (FAC_S3D_CONCURRENT=1): alone in a process the concurrent
-    # branches measured 21.4k -> 23.3k clips/s (round 2, before the kernel
-    # work below them), but after the CViT bench in the same process the very
-    # same graph ran at 20.5k vs 24.9k serial -- the branch streams come from
-    # torch's stream pool and share the process's 4 hardware queues with
-    # whatever streams exist, so the overlap is not dependable.
-    concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "0") == "1"
+    # The side streams are high-priority ones (torch's priority pool): with
+    # normal-priority pool streams the concurrent graph ran at 20.5k clips/s
+    # after the CViT bench in the same process vs 24.9k serial (they shared
+    # hardware queues with the streams already in use); with priority -1 it
+    # runs at 26.9k vs 26.1k serial there.  FAC_S3D_CONCURRENT=0: serial.
+    concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "1") == "1"
 
     def _branch_streams(self, device: torch.device):
         """Three side streams (per device) for the Inception branches."""
         streams = getattr(self, "_side", None)
         if streams is None or streams[0].device != device:
-            streams = [torch.cuda.Stream(device) for _ in range(3)]
+            prio = int(os.environ.get("FAC_S3D_SIDE_PRIORITY", "-1"))
+            streams = [torch.cuda.Stream(device, priority=prio) for _ in range(3)]
             self._side = streams
         return streams
 
