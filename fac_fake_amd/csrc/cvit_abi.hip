@@ -134,6 +134,7 @@ struct fac_ctx {
   int* errflag = nullptr;
   int* sched = nullptr;  // 2 ints: stem224 dynamic box counter + finished-workgroup count
   int stem_dynamic = 1;  // option "stem_dynamic": stem224 claims boxes from `sched` (else static)
+  int stem_nwg = 0;      // option "stem_nwg": persistent stem workgroups (0 = one per CU)
   // option "stem_events": hipEvent pairs around every fused-stem launch (the
   // bench's timed region), read back by fac_stem_event_ms
   bool stem_ev = false;
@@ -511,7 +512,8 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
         HIP_TRY(c, hipEventRecord(sev0, st));
       }
       HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_wp, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
-                                c->conv[1].b, cur, nb, c->num_cu, st, c->stem_dynamic ? c->sched : nullptr));
+                                c->conv[1].b, cur, nb, c->stem_nwg > 0 ? c->stem_nwg : c->num_cu, st,
+                                c->stem_dynamic ? c->sched : nullptr));
       if (sev1) HIP_TRY(c, hipEventRecord(sev1, st));
       MARK(0);
       l0 = 2;
@@ -696,6 +698,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   }
   if (k == "stem_dynamic") {
     c->stem_dynamic = value != 0;
+    return FAC_OK;
+  }
+  if (k == "stem_nwg") {
+    if (value < 0) return set_err(c, FAC_ERR_ARG, "stem_nwg must be >= 0");
+    c->stem_nwg = value;
     return FAC_OK;
   }
   static const char* gemm_keys[6] = {"gemm_patch", "gemm_qkv", "gemm_out", "gemm_ff1", "gemm_ff2", "gemm_head"};
