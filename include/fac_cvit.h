@@ -173,7 +173,8 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * conv stem, fac_forward_features only), "tail_priority", "stem_events" (1 =
  * time every fused-stem launch, fac_stem_event_ms), "stem_dynamic" (1 =
  * the fused stem claims boxes from a device counter, the default; 0 = static
- * box schedule), "ffn_ln_eps_exp" (n:
+ * box schedule), "stem_nwg" (persistent fused-stem workgroups; 0 = one per
+ * CU, the default), "ffn_ln_eps_exp" (n:
  * the FeedForward PreNorm LayerNorm uses eps = 10^-n; default 5, the RepBn8
  * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48). */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);

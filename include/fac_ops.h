@@ -45,7 +45,11 @@ extern "C" {
  * bias: fp32 [cout_pad] (BN shift folded in).
  * out: row m = ((n*Do + z)*Ho + y)*Wo + x, element [m*ldo + c_off + c];
  *   c_off lets Inception branches write straight into their concat slot.
- * residual (FAC_CONV_RESID): 16-bit [m*ldr + r_off + c]. */
+ * residual (FAC_CONV_RESID): 16-bit [m*ldr + r_off + c].
+ * Shapes with a dedicated kernel are routed to it inside this call (same
+ * contract): the 4x4/1 16->64 conv over space-to-depth cells (conv_s2d4:
+ * ResNet-50's / S3D's first conv) and temporal (kd,1,1) convs with 8 output
+ * frames over 16-aligned maps, cin % 64 == 0, cout % 64 == 0 (conv_tk). */
 typedef struct fac_conv_desc {
   int dtype;
   const void* in;
@@ -147,8 +151,9 @@ int fac_ggca(int dtype, const void* x, int n, int h, int w, int c, int groups, c
  * (+ MaxPool2d(2,2) if pool) — cvit.py:86-148 — on the halo-staged implicit
  * GEMM of conv.hip: in [n][h][h][cin] -> out [n][h'][h'][cout] (h' = h/2 with
  * pool); h in {112, 56, 28, 14} (224: cout 32, the unfused kernel), cin a
- * multiple of 32, cout a multiple of the resolution's block (64 at 112, 128
- * at 56 and 14, 256 at 28).  wpk: fac_conv3x3_pack of the folded fp32 weight
+ * multiple of 32, cout a multiple of one of the resolution's blocks (64 at
+ * 112; 128 or 64 at 56; 256, 192 or 128 at 28; 128 at 14 — the largest that
+ * divides cout is used).  wpk: fac_conv3x3_pack of the folded fp32 weight
  * [cout][cin][3][3]; bias fp32 [cout]; zero256: 256 zero bytes of device
  * memory (the source of zero-padding loads).
  * fac_conv3x3_packed_elems: 16-bit elements of the packed weight (0: shape
