@@ -336,9 +336,11 @@ __global__ __launch_bounds__(256) void pack_input_s2d(const void* src, int n_img
                                                       int pa, float div, float m0, float m1, float m2, float s0,
                                                       float s1, float s2, uint16_t* out) {
   const int Ho = H / 2 + pb + pa, Wo = W / 2 + pb + pa;
-  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (long long)n_img * Ho * Wo) return;
-  const int X = (int)(t % Wo), Y = (int)((t / Wo) % Ho), n = (int)(t / ((long long)Wo * Ho));
+  // 32-bit index math (the launcher checks n_img * Ho * Wo < 2^31): a 64-bit
+  // division per cell cost as much as the loads
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_img * Ho * Wo) return;
+  const int nY = t / Wo, X = t - nY * Wo, n = nY / Ho, Y = nY - n * Ho;
   const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
   u16x8 lo = (u16x8)0, hi = (u16x8)0;
   const int y0 = 2 * (Y - pb), x0 = 2 * (X - pb);
@@ -913,6 +915,7 @@ int fac_pack_input_s2d(int dtype, const void* src, int src_kind, int n, int fram
   const float sd[3] = {std3 ? std3[0] : 1.f, std3 ? std3[1] : 1.f, std3 ? std3[2] : 1.f};
   const long long total =
       (long long)n * frames * (h / 2 + pad_before + pad_after) * (w / 2 + pad_before + pad_after);
+  if (total >= (1LL << 31) - 256) return FAC_ERR_SHAPE;  // the kernel indexes cells in 32 bits
   const int nb = (int)((total + 255) / 256);
   hipStream_t st = (hipStream_t)stream;
   uint16_t* o = (uint16_t*)out;

@@ -137,12 +137,14 @@ class S3D(nn.Module):
         self._prep = (idx, v)
 
     # ------------------------------------------------------------------ forward
-    # The side streams are high-priority ones (torch's priority pool): with
-    # normal-priority pool streams the concurrent graph ran at 20.5k clips/s
-    # after the CViT bench in the same process vs 24.9k serial (they shared
-    # hardware queues with the streams already in use); with priority -1 it
-    # runs at 26.9k vs 26.1k serial there.  FAC_S3D_CONCURRENT=0: serial.
-    concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "1") == "1"
+    # Opt-in (FAC_S3D_CONCURRENT=1, side-stream priority FAC_S3D_SIDE_PRIORITY,
+    # default -1).  Whether the overlap pays depends on which of the process's
+    # four hardware queues torch's pool streams land on, i.e. on the process's
+    # stream history: normal-priority side streams ran the graph at 27.0k
+    # clips/s alone in a process but 20.5k after the CViT bench (serial 24.9k);
+    # priority -1 gave 27.2k after the CViT bench (serial 26.2k) but 20.8k
+    # alone.  Serial is the dependable default.
+    concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "0") == "1"
 
     def _branch_streams(self, device: torch.device):
         """Three side streams (per device) for the Inception branches."""
