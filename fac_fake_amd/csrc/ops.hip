@@ -23,6 +23,7 @@
 // (bias, ReLU, residual, ReLU, convert), so a row's BN channels leave in one
 // contiguous burst.
 #include <algorithm>
+#include <climits>
 
 #include "common.hpp"
 #include "fac_cvit.h"
@@ -44,6 +45,9 @@ struct ConvP {
   int ldo, c_off, ldr, r_off, flags;
   int vec_out, vec_res;
   int M;
+  void* out1;  // column segments of fac_conv_nd_split (split1 = split2 = INT_MAX: one output)
+  void* out2;
+  int ldo1, ldo2, split1, split2;
 };
 
 // (channel piece, tap) of one K piece, advanced in place by 4 pieces
@@ -243,7 +247,12 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
       float* o = (float*)p.out + (size_t)mo * p.ldo + p.c_off + c;
       for (int k = 0; k < nc; ++k) o[k] = v[k];
     } else {
-      uint16_t* o = (uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c;
+      // column segments (fac_conv_nd_split): [0, split1) -> out (ldo, c_off),
+      // [split1, split2) -> out1 (ldo1), [split2, cout) -> out2 (ldo2)
+      uint16_t* o;
+      if (c >= p.split2) o = (uint16_t*)p.out2 + (size_t)mo * p.ldo2 + (c - p.split2);
+      else if (c >= p.split1) o = (uint16_t*)p.out1 + (size_t)mo * p.ldo1 + (c - p.split1);
+      else o = (uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c;
       if (p.vec_out && nc == 8) {
         const u16x4 a = T::pack4((f32x4){v[0], v[1], v[2], v[3]});
         const u16x4 b = T::pack4((f32x4){v[4], v[5], v[6], v[7]});
@@ -759,7 +768,8 @@ int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_
   return FAC_OK;
 }
 
-int fac_conv_nd(const fac_conv_desc* d, void* stream) {
+static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1, void* out2, int ldo2, int split2,
+                        void* stream) {
   using namespace fac;
   if (!d || !d->in || !d->weight || !d->out) return FAC_ERR_ARG;
   if (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16) return FAC_ERR_ARG;
@@ -774,7 +784,7 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   int cout_pad, k_pad;
   fac_conv_weight_layout(d->cout, d->cin, d->kd, d->kh, d->kw, &cout_pad, &k_pad);
   if (d->k_pad != k_pad) return FAC_ERR_SHAPE;
-  if (d->ldo < d->c_off + d->cout || d->c_off < 0) return FAC_ERR_SHAPE;
+  if (d->ldo < d->c_off + std::min(d->cout, split1) || d->c_off < 0) return FAC_ERR_SHAPE;
   if ((d->flags & FAC_CONV_RESID) && (!d->residual || d->ldr < d->r_off + d->cout || d->r_off < 0)) return FAC_ERR_ARG;
   const long long M = (long long)d->n * d->od * d->oh * d->ow;
   if (M >= (1LL << 31) || (long long)d->n * d->d * d->h * d->w * d->cin >= (1LL << 40)) return FAC_ERR_SHAPE;
@@ -812,10 +822,18 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   p.vec_out = (d->ldo % 8 == 0 && d->c_off % 8 == 0) ? 1 : 0;
   p.vec_res = (d->ldr % 8 == 0 && d->r_off % 8 == 0) ? 1 : 0;
   p.M = (int)M;
+  p.out1 = out1;
+  p.out2 = out2;
+  p.ldo1 = ldo1;
+  p.ldo2 = ldo2;
+  p.split1 = split1;
+  p.split2 = split2;
+  const bool split = split1 < d->cout;
+  if (split) p.vec_out = p.vec_out && ldo1 % 8 == 0 && ldo2 % 8 == 0;
   hipStream_t st = (hipStream_t)stream;
   // the space-to-depth first conv (4x4/1 over 16-channel cells, cout 64, no
   // residual, dense output): its own kernel (conv_s2d4)
-  if (d->kd == 1 && d->kh == 4 && d->kw == 4 && d->sd == 1 && d->sh == 1 && d->sw == 1 && d->pd == 0 && d->ph == 0 &&
+  if (!split && d->kd == 1 && d->kh == 4 && d->kw == 4 && d->sd == 1 && d->sh == 1 && d->sw == 1 && d->pd == 0 && d->ph == 0 &&
       d->pw == 0 && d->cin == 16 && d->cout == 64 && k_pad == 256 && d->oh % 8 == 0 && d->ow % 28 == 0 &&
       d->ldo == 64 && d->c_off == 0 && (d->flags & ~FAC_CONV_RELU) == 0) {
     const int nimg = d->n * d->od, nbox = nimg * (d->oh / 8) * (d->ow / 28);
@@ -834,7 +852,7 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   }
   // S3D's temporal (kd,1,1) convs with 8 output frames over 16-aligned
   // spatial maps: conv_tk (LDS slab per 16 positions, weights resident)
-  if (d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 && d->pw == 0 && d->od == 8 &&
+  if (!split && d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 && d->pw == 0 && d->od == 8 &&
       d->cin % 64 == 0 && d->cout % 64 == 0 && (d->h * d->w) % 16 == 0 && d->ldo % 4 == 0 && d->c_off % 4 == 0 &&
       (d->flags & ~FAC_CONV_RELU) == 0 && k_pad == d->kd * d->cin) {
     const int ks = d->kd * d->cin / 32, slab = d->d * 16 * d->cin;
@@ -860,6 +878,19 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   }
   const hipError_t e = d->dtype == FAC_DTYPE_BF16 ? launch_convnd<BF16>(p, cout_pad, st) : launch_convnd<F16>(p, cout_pad, st);
   return e == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_conv_nd(const fac_conv_desc* d, void* stream) {
+  return conv_nd_impl(d, nullptr, 0, INT_MAX, nullptr, 0, INT_MAX, stream);
+}
+
+int fac_conv_nd_split(const fac_conv_desc* d, void* out1, int ldo1, int split1, void* out2, int ldo2, int split2,
+                      void* stream) {
+  if (!d || !out1 || !out2 || split1 <= 0 || split1 % 8 || split2 <= split1 || split2 % 8 || split2 >= d->cout ||
+      ldo1 < split2 - split1 || ldo2 < d->cout - split2 || (d->flags & (FAC_CONV_RESID | FAC_CONV_OUT_F32)) ||
+      d->ldo < d->c_off + split1)
+    return FAC_ERR_ARG;
+  return conv_nd_impl(d, out1, ldo1, split1, out2, ldo2, split2, stream);
 }
 
 int fac_pool_nd(const fac_pool_desc* d, void* stream) {

@@ -208,6 +208,35 @@ class ConvLayer:
         return out
 
 
+def conv_split(layer: ConvLayer, x: torch.Tensor, splits, out0: torch.Tensor, c_off0: int, out1: torch.Tensor,
+               out2: torch.Tensor, relu: bool = True) -> None:
+    """One fac_conv_nd_split launch of `layer` (a conv over concatenated
+    output channels): columns [0, s1) -> out0[..., c_off0:], [s1, s2) -> out1,
+    [s2, cout) -> out2 (each [N,D,H,W,C] contiguous)."""
+    s1, s2 = splits
+    n, d, h, w, c = x.shape
+    if c != layer.cin_p or x.dtype != TORCH16[layer.dtype] or not x.is_contiguous():
+        raise ValueError("conv_split input must be a contiguous 16-bit [N,D,H,W,cin] tensor")
+    od, oh, ow = layer.out_dims(d, h, w)
+    for t, width in ((out1, s2 - s1), (out2, layer.cout - s2)):
+        if tuple(t.shape[:4]) != (n, od, oh, ow) or t.shape[4] < width or not t.is_contiguous():
+            raise ValueError("conv_split outputs must be contiguous [N,D,H,W,C] tensors wide enough")
+    g = layer.g
+    dsc = ConvDesc()
+    dsc.dtype = _lib.DTYPES[layer.dtype]
+    dsc.inp = x.data_ptr()
+    dsc.n, dsc.d, dsc.h, dsc.w, dsc.cin = n, d, h, w, c
+    dsc.weight, dsc.bias = layer.w.data_ptr(), layer.b.data_ptr()
+    dsc.cout, dsc.k_pad = layer.cout, layer.k_pad
+    dsc.kd, dsc.kh, dsc.kw, dsc.sd, dsc.sh, dsc.sw = g.kd, g.kh, g.kw, g.sd, g.sh, g.sw
+    dsc.pd, dsc.ph, dsc.pw = g.pd, g.ph, g.pw
+    dsc.od, dsc.oh, dsc.ow = od, oh, ow
+    dsc.out, dsc.ldo, dsc.c_off = out0.data_ptr(), out0.shape[4], c_off0
+    dsc.flags = RELU if relu else 0
+    _lib.check(_lib.load().fac_conv_nd_split(ctypes.byref(dsc), out1.data_ptr(), out1.shape[4], s1, out2.data_ptr(),
+                                             out2.shape[4], s2, _stream(x)), None, "fac_conv_nd_split")
+
+
 def pool(x: torch.Tensor, kernel, stride, padding=0, mode: str = "max", out: torch.Tensor | None = None,
          c_off: int = 0) -> torch.Tensor:
     n, d, h, w, c = x.shape

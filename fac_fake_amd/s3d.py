@@ -29,7 +29,7 @@ from torch import nn
 
 from . import _lib
 from .cvit import _Node
-from .ops import TORCH16, ConvLayer, fold_bn, max_pool_sep, pack_input, pack_input_s2d, pool, s2d_weight, sigmoid
+from .ops import TORCH16, ConvLayer, conv_split, fold_bn, max_pool_sep, pack_input, pack_input_s2d, pool, s2d_weight, sigmoid
 from .weights import s3d_base, s3d_param_specs
 
 BN_EPS = 1e-3   # BatchNorm3d(eps=1e-3) in BasicConv3d / SepConv3d (model.py:54,67,71)
@@ -129,9 +129,18 @@ class S3D(nn.Module):
                 self._layers.append(("pool", L[1:]))
             else:
                 cin, b0, (b1a, b1b), (b2a, b2b), b3 = L[1:]
+                # the three 1x1x1 heads reading the block input (branch0.0,
+                # branch1.0, branch2.0) also as ONE conv over their
+                # concatenated output channels (ops.conv_split)
+                heads = [fold_bn(sd[f"{h}.conv.weight"], None, sd[f"{h}.bn.weight"], sd[f"{h}.bn.bias"],
+                                 sd[f"{h}.bn.running_mean"], sd[f"{h}.bn.running_var"], BN_EPS)
+                         for h in (f"{p}.branch0.0", f"{p}.branch1.0", f"{p}.branch2.0")]
+                merged = ConvLayer(torch.cat([h[0] for h in heads]), torch.cat([h[1] for h in heads]), 1, 0,
+                                   dtype=dt, device=device)
                 self._layers.append(("mixed", dict(
                     b0=bconv(f"{p}.branch0.0"), b1a=bconv(f"{p}.branch1.0"), b1=sep(f"{p}.branch1.1", 3, 1, 1),
                     b2a=bconv(f"{p}.branch2.0"), b2=sep(f"{p}.branch2.1", 3, 1, 1), b3=bconv(f"{p}.branch3.1"),
+                    heads=merged, head_splits=(b0, b0 + b1a), head_widths=(b1a, b2a),
                     widths=(b0, b1b, b2b, b3))))
         self._fc = ConvLayer(sd["fc.0.weight"], sd["fc.0.bias"], 1, 0, dtype=dt, device=device)
         self._prep = (idx, v)
@@ -145,6 +154,8 @@ class S3D(nn.Module):
     # priority -1 gave 27.2k after the CViT bench (serial 26.2k) but 20.8k
     # alone.  Serial is the dependable default.
     concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "0") == "1"
+    # serial order: the three 1x1x1 heads as one column-split launch (ops.conv_split)
+    merged_heads = os.environ.get("FAC_S3D_MERGED_HEADS", "1") == "1"
 
     def _branch_streams(self, device: torch.device):
         """Three side streams (per device) for the Inception branches."""
@@ -170,12 +181,24 @@ class S3D(nn.Module):
         o2 = o1 + blk["widths"][1]
         o3 = o2 + blk["widths"][2]
         main = torch.cuda.current_stream(x.device)
-        if not self.concurrent_branches:
+        if not self.concurrent_branches and not self.merged_heads:
             s1, t1 = blk["b1"]
             s2, t2 = blk["b2"]
             blk["b0"](x, out=out, c_off=0)
             t1(s1(blk["b1a"](x)), out=out, c_off=o1)
             t2(s2(blk["b2a"](x)), out=out, c_off=o2)
+            blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
+            return out
+        if not self.concurrent_branches:
+            s1, t1 = blk["b1"]
+            s2, t2 = blk["b2"]
+            # branch0 into its slot, branch1.0 / branch2.0 into their own
+            # tensors: one launch (column-split GEMM) instead of three
+            h1 = torch.empty(n, d, h, w, blk["head_widths"][0], dtype=x.dtype, device=x.device)
+            h2 = torch.empty(n, d, h, w, blk["head_widths"][1], dtype=x.dtype, device=x.device)
+            conv_split(blk["heads"], x, blk["head_splits"], out, 0, h1, h2)
+            t1(s1(h1), out=out, c_off=o1)
+            t2(s2(h2), out=out, c_off=o2)
             blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
             return out
         side = self._branch_streams(x.device)

@@ -70,6 +70,16 @@ typedef struct fac_conv_desc {
 
 int fac_conv_nd(const fac_conv_desc* desc, void* stream);
 
+/* fac_conv_nd whose output columns go to three tensors: [0, split1) to
+ * desc->out (ldo, c_off), [split1, split2) to out1 (row stride ldo1, from
+ * column 0), [split2, cout) to out2 (ldo2).  For convs that share an input,
+ * e.g. the three 1x1x1 heads of an S3D Inception block (model.py:84-342:
+ * branch0, branch1.0, branch2.0) as one GEMM over concatenated weights:
+ * every output column is computed exactly as by its own launch.  Splits are
+ * multiples of 8; no residual, no fp32 output. */
+int fac_conv_nd_split(const fac_conv_desc* desc, void* out1, int ldo1, int split1, void* out2, int ldo2, int split2,
+                      void* stream);
+
 /* Weight packing geometry for fac_conv_nd: *cout_pad = cout rounded up to
  * 128, *k_pad = taps*cin rounded up to 64. */
 int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad);

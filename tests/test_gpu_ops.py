@@ -261,3 +261,25 @@ def test_s3d_graph_replay_matches_eager(s3d_models):
     gr.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, eager)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+def test_conv_split_equals_separate_convs(dt):
+    """fac_conv_nd_split over concatenated weights (S3D's merged Inception
+    heads) writes exactly what three separate fac_conv_nd launches write."""
+    from fac_fake_amd.ops import ConvLayer, conv_split
+    g = torch.Generator().manual_seed(11)
+    n, d, h, w, cin, widths = 2, 4, 7, 7, 480, (192, 96, 16)
+    x = torch.randn(n, d, h, w, cin, generator=g).to(T16[dt]).to(DEV)
+    ws = [torch.randn(c, cin, 1, 1, 1, generator=g) / np.sqrt(cin) for c in widths]
+    bs = [torch.randn(c, generator=g) * 0.1 for c in widths]
+    sep = [ConvLayer(wi, bi, 1, 0, dtype=dt, device=DEV) for wi, bi in zip(ws, bs)]
+    merged = ConvLayer(torch.cat(ws), torch.cat(bs), 1, 0, dtype=dt, device=DEV)
+    out = torch.zeros(n, d, h, w, 512, dtype=T16[dt], device=DEV)
+    h1 = torch.empty(n, d, h, w, widths[1], dtype=T16[dt], device=DEV)
+    h2 = torch.empty(n, d, h, w, widths[2], dtype=T16[dt], device=DEV)
+    conv_split(merged, x, (widths[0], widths[0] + widths[1]), out, 0, h1, h2)
+    r0, r1, r2 = (layer(x) for layer in sep)
+    torch.cuda.synchronize()
+    assert torch.equal(out[..., :widths[0]], r0) and out[..., widths[0]:].abs().max() == 0
+    assert torch.equal(h1, r1) and torch.equal(h2, r2)
