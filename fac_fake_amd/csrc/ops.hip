@@ -24,6 +24,7 @@
 // contiguous burst.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "fac_cvit.h"
@@ -48,6 +49,7 @@ struct ConvP {
   void* out1;  // column segments of fac_conv_nd_split (split1 = split2 = INT_MAX: one output)
   void* out2;
   int ldo1, ldo2, split1, split2;
+  int ny;  // column tiles when the grid is flat (gridDim.y == 1, ny > 1), else 0
 };
 
 // (channel piece, tap) of one K piece, advanced in place by 4 pieces
@@ -96,9 +98,15 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  int bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);  // XCD-contiguous row tiles
-  const int m0 = bx * BM, n0 = blockIdx.y * BN;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);  // XCD-contiguous tiles
+  if (p.ny) {
+    // flat grid: the ny column tiles of one row tile are consecutive on one
+    // XCD, so they share the row tile's A gather through that XCD's L2
+    by = bx % p.ny;
+    bx /= p.ny;
+  }
+  const int m0 = bx * BM, n0 = by * BN;
 
   // LDS images: rows of 64 k (128 B), the 16-byte piece j of row r at position
   // j ^ ((r >> 1) & 7) (conflict-free ds_read_b128, as in transformer.hip's
@@ -637,6 +645,137 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
 }
 
 
+// ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128} — ResNet-50's
+// bottleneck expansions (conv3 64 -> 256 / 128 -> 512 + residual + ReLU,
+// ResVitKan.py:187's torchvision resnet50 layer1/layer2), their downsample
+// 1x1s and layer1's 64 -> 64 reductions.  Through the generic implicit GEMM
+// these are HBM-bound with one or two K steps per 128-row tile, so every
+// workgroup is a serial load -> MFMA -> LDS-staged store chain and the chip
+// holds too few bytes in flight.  Here a persistent workgroup keeps its
+// 64-column weight block in LDS and walks row tiles of 64 * RT positions:
+// the next tile's rows stream into the other LDS buffer (glds) while this
+// tile computes and stores, and so does its residual block (RES; read into
+// registers before the barrier that frees the buffer).  MFMAs transposed (rows = channels) as in conv_s2d4: each lane ends
+// with 4 channels of one position and stores 8 bytes from registers.
+// A rows (K / 8 16-byte pieces) keep piece p at p ^ (row & 7).
+template <class T, int KC, int RT, bool RES>
+__global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                  const float* __restrict__ bias, const uint16_t* __restrict__ res,
+                                                  uint16_t* __restrict__ out, int M, int kp, int ldo, int c_off,
+                                                  int ldr, int r_off, int flags) {
+  constexpr int K = KC * 32, PPR = K / 8, BM = 64 * RT;
+  constexpr int WEL = 64 * K, AEL = BM * K;
+  constexpr int PER = BM * PPR / 256;  // glds per lane per tile
+  constexpr int REL = RES ? BM * 64 : 0, RPER = RES ? BM / 32 : 0;  // residual tile elements, glds
+  static_assert(PER * 256 == BM * PPR, "tile pieces");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * AEL + 2 * REL];
+  uint16_t* const sw = smem;
+  uint16_t* const sa = smem + WEL;
+  uint16_t* const sr = sa + 2 * AEL;  // residual tiles, rows of 8 pieces, piece p at p ^ (row & 7)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int n0 = blockIdx.y * 64;
+  const bool relu_on = flags & FAC_CONV_RELU, relu2 = flags & FAC_CONV_RELU2;
+
+  // weights [s][ct][g][r16][8]: one contiguous 1 KB fragment per (k-step, channel tile)
+  for (int c = tid; c < 64 * PPR; c += 256) {
+    const int n = c / PPR, k8 = c - n * PPR;
+    *(u16x8*)(sw + ((((k8 >> 2) * 4 + (n >> 4)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+        *(const u16x8*)(w + (size_t)(n0 + n) * kp + k8 * 8);
+  }
+  float bv[4][4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[n0 + ct * 16 + 4 * g + j] : 0.f;
+  // this lane's glds slots: row and (logical) piece, fixed across tiles
+  int arow[PER], aoff[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int q = (i * 4 + wave) * 64 + lane, r = q / PPR, pp = q - r * PPR;
+    arow[i] = r;
+    aoff[i] = (pp ^ (r & 7)) * 8;
+  }
+  // a tile's A rows, then (RES) its 64-column residual block, into buffer buf
+  auto issue = [&](int tile, int buf) {
+    const int m0 = tile * BM;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int m = m0 + arow[i];
+      glds16(m < M ? in + (size_t)m * K + aoff[i] : g_zero16, sa + buf * AEL + (i * 4 + wave) * 64 * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < RPER; ++i) {
+      const int q = (i * 4 + wave) * 64 + lane, r = q >> 3, m = m0 + r;
+      glds16(m < M ? res + (size_t)m * ldr + r_off + n0 + (((q & 7) ^ (r & 7)) << 3) : g_zero16,
+             sr + buf * REL + (i * 4 + wave) * 64 * 8);
+    }
+  };
+  __syncthreads();  // weights in
+  const int ntiles = (M + BM - 1) / BM;
+  int t = blockIdx.x;
+  if (t < ntiles) issue(t, 0);
+  for (int it = 0; t < ntiles; ++it, t += gridDim.x) {
+    const int buf = it & 1;
+    const int mrow = t * BM + wave * RT * 16 + r16;  // this lane's position in row tile 0
+    if (t + (int)gridDim.x < ntiles) {
+      issue(t + gridDim.x, buf ^ 1);  // its buffer's readers passed the previous tile's barrier
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PER + RPER) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // residual vectors to registers before the barrier that frees the buffer
+    u16x4 rv[RT][4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int r = (wave * RT + rt) * 16 + r16;
+        rv[rt][ct] = RES ? *(const u16x4*)(sr + buf * REL + r * 64 + (((ct * 2 + (g >> 1)) ^ (r & 7)) << 3) + (g & 1) * 4)
+                         : (u16x4)0;
+      }
+    const uint16_t* a = sa + buf * AEL;
+    f32x4 acc[RT][4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) acc[rt][ct] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      u16x8 wf[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) wf[ct] = *(const u16x8*)(sw + (((s * 4 + ct) * 4 + g) * 16 + r16) * 8);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = (wave * RT + rt) * 16 + r16;
+        const u16x8 pf = *(const u16x8*)(a + (r * PPR + ((s * 4 + g) ^ (r & 7))) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[rt][ct] = T::mfma(wf[ct], pf, acc[rt][ct]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffers free for the tile after next
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int m = mrow + rt * 16;
+      if (m >= M) continue;
+      uint16_t* o = out + (size_t)m * ldo + c_off + n0 + 4 * g;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float x = acc[rt][ct][j] + bv[ct][j];
+          if (relu_on) x = relu(x);
+          if constexpr (RES) x += T::to_f32(rv[rt][ct][j]);
+          if (relu2) x = relu(x);
+          v[j] = x;
+        }
+        *(u16x4*)(o + ct * 16) = T::pack4(v);
+      }
+    }
+  }
+}
+
 // ---- conv_tk: S3D's temporal (kd,1,1) convs with 8 output frames (model.py:
 // 63-82, SepConv3d's conv_t + bn_t + relu_t: base.0's (7,1,1)/(2,1,1) and
 // base.3's (3,1,1) at 56^2 / 28^2 positions).  Through the generic implicit
@@ -734,25 +873,44 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
   }
 }
 
+// grid of gx row tiles x ny column tiles: flat (column tiles of a row tile
+// adjacent, see convnd_igemm) unless FAC_CONV_FLAT=0 or it would overflow
+static dim3 conv_grid(ConvP& p, int gx, int ny) {
+  static const bool flat = [] {
+    const char* e = std::getenv("FAC_CONV_FLAT");
+    return !(e && e[0] == '0');
+  }();
+  if (flat && ny > 1 && (long long)gx * ny < INT_MAX) {
+    p.ny = ny;
+    return dim3(gx * ny, 1);
+  }
+  p.ny = 0;
+  return dim3(gx, ny);
+}
+
 template <class T>
-static hipError_t launch_convnd(const ConvP& p, int cout_pad, hipStream_t st) {
+static hipError_t launch_convnd(ConvP p, int cout_pad, hipStream_t st) {
   (void)cout_pad;
   const int gx64 = (p.M + 63) / 64, gx128 = (p.M + 127) / 128, gx256 = (p.M + 255) / 256;
   const int ny64 = (p.Cout + 63) / 64, ny128 = (p.Cout + 127) / 128;
   if (p.ksteps <= 2) {
     // K <= 128 (1x1 expansions): memory-bound, so occupancy first — a 2-slot
     // ring (48 KB) lets three 128 x 64 workgroups share a CU
-    convnd_igemm<T, 128, 64, 2, 2, 3, 2><<<dim3(gx128, ny64), 256, 0, st>>>(p);
+    const dim3 g = conv_grid(p, gx128, ny64);
+    convnd_igemm<T, 128, 64, 2, 2, 3, 2><<<g, 256, 0, st>>>(p);
   } else if ((long long)gx128 * ny64 < 512) {
     // small grids (S3D's late 4x7x7 / 2x3x3 stages): 64 x 64 tiles, three per CU
-    convnd_igemm<T, 64, 64, 2, 2, 3, 3><<<dim3(gx64, ny64), 256, 0, st>>>(p);
+    const dim3 g = conv_grid(p, gx64, ny64);
+    convnd_igemm<T, 64, 64, 2, 2, 3, 3><<<g, 256, 0, st>>>(p);
   } else if (p.Cout % 128 == 0 && (long long)gx256 * ny128 >= 448) {
     // 256 x 128 tiles (8 waves, 144 KB ring, one per CU: 48 KB global -> LDS per
     // 4.2 MFLOP, twice the 128 x 64 tile's intensity) when the grid still fills
     // the chip about twice over and no column tile is half empty
-    convnd_igemm<T, 256, 128, 4, 2, 1, 3><<<dim3(gx256, ny128), 512, 0, st>>>(p);
+    const dim3 g = conv_grid(p, gx256, ny128);
+    convnd_igemm<T, 256, 128, 4, 2, 1, 3><<<g, 512, 0, st>>>(p);
   } else {
-    convnd_igemm<T, 128, 64, 2, 2, 2, 3><<<dim3(gx128, ny64), 256, 0, st>>>(p);
+    const dim3 g = conv_grid(p, gx128, ny64);
+    convnd_igemm<T, 128, 64, 2, 2, 2, 3><<<g, 256, 0, st>>>(p);
   }
   return hipGetLastError();
 }
@@ -848,6 +1006,48 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     else
       conv_s2d4<F16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
                                            (uint16_t*)d->out, nbox, d->h, d->w, d->oh, d->ow, k_pad, relu_on);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  // stride-1 1x1 convs with K = cin in {64, 128}: conv_pw
+  static const bool pw_on = [] {
+    const char* e = std::getenv("FAC_CONV_PW");
+    return !(e && e[0] == '0');
+  }();
+  if (pw_on && !split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+      d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->cin == 64 || d->cin == 128) && k_pad == d->cin &&
+      d->cout % 64 == 0 && d->ldo % 4 == 0 && d->c_off % 4 == 0 && !(d->flags & FAC_CONV_OUT_F32) &&
+      (!(d->flags & FAC_CONV_RESID) || (d->ldr % 8 == 0 && d->r_off % 8 == 0))) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+    const bool r = d->flags & FAC_CONV_RESID;
+    const int ny = d->cout / 64;
+    // rows per tile and the LDS-bound residency: weights 64 x cin, two A
+    // buffers of bm x cin (+ two residual blocks of bm x 64), 160 KB per CU
+    const int bm = d->cin == 64 ? 128 : 64;
+    const int lds = 128 * d->cin + 4 * bm * d->cin + (r ? 256 * bm : 0);
+    const int occ = std::min(3, 163840 / lds);
+    const int ntiles = (int)((M + bm - 1) / bm);
+    // one persistent workgroup per resident slot over all column blocks, a
+    // multiple of 8 row slots so a row tile's column blocks share an XCD
+    int gx = std::max(8, (occ * ncu / ny) / 8 * 8);
+    gx = std::min(gx, ntiles);
+    const dim3 grid(gx, ny);
+    const uint16_t* res = (const uint16_t*)d->residual;
+    uint16_t* o = (uint16_t*)d->out;
+    const uint16_t* in = (const uint16_t*)d->in;
+    const uint16_t* wt = (const uint16_t*)d->weight;
+    const int mi = (int)M;
+#define FAC_PW(TT, KC, RT, R) \
+  conv_pw<TT, KC, RT, R><<<grid, 256, 0, st>>>(in, wt, d->bias, res, o, mi, k_pad, d->ldo, d->c_off, d->ldr, d->r_off, d->flags)
+    if (d->dtype == FAC_DTYPE_BF16) {
+      if (d->cin == 64) r ? FAC_PW(BF16, 2, 2, true) : FAC_PW(BF16, 2, 2, false);
+      else r ? FAC_PW(BF16, 4, 1, true) : FAC_PW(BF16, 4, 1, false);
+    } else {
+      if (d->cin == 64) r ? FAC_PW(F16, 2, 2, true) : FAC_PW(F16, 2, 2, false);
+      else r ? FAC_PW(F16, 4, 1, true) : FAC_PW(F16, 4, 1, false);
+    }
+#undef FAC_PW
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   // S3D's temporal (kd,1,1) convs with 8 output frames over 16-aligned

@@ -60,6 +60,9 @@ CONV_CASES = [
     # the space-to-depth first conv (ops.hip conv_s2d4: 4x4/1, 16 -> 64, 8 x 28 boxes)
     (2, 2, 19, 31, 16, 64, (1, 4, 4), 1, 0),
     (1, 1, 59, 59, 16, 64, (1, 4, 4), 1, 0),
+    # stride-1 1x1 convs with cin 64 / 128 (ops.hip conv_pw; case 0 too)
+    (3, 1, 23, 29, 128, 192, (1, 1, 1), 1, 0),
+    (1, 1, 56, 56, 64, 256, (1, 1, 1), 1, 0),
 ]
 
 
@@ -82,6 +85,32 @@ def test_conv_nd_vs_torch_fp32(case, dt):
     assert tuple(y.shape) == tuple(yr.shape)
     assert u.max() <= 1.0, (case, float(u.max()))
     assert (u > 0).float().mean() <= 0.05
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("cin,cout", [(64, 256), (128, 512)])
+def test_conv_pw_residual_into_slot(cin, cout, dt):
+    """conv_pw's bottleneck epilogue relu(relu(conv + b) + res) written into
+    a channel slot of a wider buffer, over enough positions (40 000, ragged
+    last tile) that every persistent workgroup walks several row tiles."""
+    from fac_fake_amd.ops import ConvLayer
+    g = torch.Generator().manual_seed(11 + cin)
+    n, h, w = 4, 100, 100
+    x = torch.randn(n, cin, 1, h, w, generator=g).to(T16[dt]).float()
+    wt = torch.randn(cout, cin, 1, 1, 1, generator=g) / np.sqrt(cin)
+    b = torch.randn(cout, generator=g) * 0.1
+    res = torch.randn(n, 1, h, w, cout, generator=g).to(T16[dt])
+    layer = ConvLayer(wt, b, 1, 0, dtype=dt, device=DEV)
+    big = torch.zeros(n, 1, h, w, cout + 16, dtype=T16[dt], device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    layer(xg, relu=True, out=big, c_off=8, residual=res.to(DEV), relu2=True)
+    torch.cuda.synchronize()
+    conv = F.conv3d(x, wt.to(T16[dt]).float(), b).permute(0, 2, 3, 4, 1)
+    ref = F.relu(F.relu(conv) + res.float()).to(T16[dt])
+    bc = big.cpu()
+    u = _ulps(bc[..., 8:8 + cout], ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05
+    assert bc[..., :8].abs().max() == 0 and bc[..., 8 + cout:].abs().max() == 0
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
