@@ -315,6 +315,66 @@ __global__ __launch_bounds__(256) void pool_nd(fac_pool_desc p, int total) {
   *(u16x8*)((uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c8 * 8) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// ---- 3x3x3 / stride-1 / pad-1 max pooling (S3D's Inception branch3,
+// model.py:84-342: MaxPool3d(3, 1, 1) before the 1x1x1 conv): one thread per
+// (clip, position, 8-channel piece) walks the frames, taking each frame's
+// 3x3 spatial max once (9 reads, the neighbours' rows shared in L1/L2) and
+// the frame max over a sliding window of three, so the map is read from HBM
+// about once and written once — one pass instead of the separable version's
+// three, bit-identical (a max selects one of its inputs either way).
+template <class T>
+__global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int C8 = p.c / 8;
+  const int c8 = t % C8, t1 = t / C8;
+  const int x = t1 % p.w, t2 = t1 / p.w;
+  const int y = t2 % p.h, n = t2 / p.h;
+  const size_t fs = (size_t)p.h * p.w * p.c;
+  const uint16_t* inb = (const uint16_t*)p.in + (size_t)n * p.d * fs + c8 * 8;
+  auto frame_max = [&](int z, float (&m)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = -__builtin_inff();
+    const uint16_t* f = inb + (size_t)z * fs;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = y + dy;
+      if ((unsigned)iy >= (unsigned)p.h) continue;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ix = x + dx;
+        if ((unsigned)ix >= (unsigned)p.w) continue;
+        const u16x8 v = *(const u16x8*)(f + ((size_t)iy * p.w + ix) * p.c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], T::to_f32(v[i]));
+      }
+    }
+  };
+  float pm[8], cm[8], nm[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pm[i] = -__builtin_inff();
+  frame_max(0, cm);
+  uint16_t* ob = (uint16_t*)p.out + ((size_t)n * p.d * p.h * p.w + (size_t)y * p.w + x) * p.ldo + p.c_off + c8 * 8;
+  for (int z = 0; z < p.d; ++z) {
+    if (z + 1 < p.d) {
+      frame_max(z + 1, nm);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) nm[i] = -__builtin_inff();
+    }
+    float a[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[i] = fmaxf(fmaxf(pm[i], cm[i]), nm[i]);
+      pm[i] = cm[i];
+      cm[i] = nm[i];
+    }
+    const u16x4 lo = T::pack4((f32x4){a[0], a[1], a[2], a[3]});
+    const u16x4 hi = T::pack4((f32x4){a[4], a[5], a[6], a[7]});
+    *(u16x8*)(ob + (size_t)z * p.h * p.w * p.ldo) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
 // ---- input staging
 template <class T, bool U8>
 __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
@@ -1103,8 +1163,22 @@ int fac_pool_nd(const fac_pool_desc* d, void* stream) {
   if (d->ldo % 8 || d->c_off % 8 || d->ldo < d->c_off + d->c) return FAC_ERR_SHAPE;
   const long long total = (long long)d->n * d->od * d->oh * d->ow * (d->c / 8);
   if (total >= (1LL << 31)) return FAC_ERR_SHAPE;
-  const int nb = (int)((total + 255) / 256);
   hipStream_t st = (hipStream_t)stream;
+  static const bool mp3 = [] {
+    const char* e = std::getenv("FAC_POOL_MAX3");
+    return !(e && e[0] == '0');
+  }();
+  if (mp3 && d->mode == 0 && d->kd == 3 && d->kh == 3 && d->kw == 3 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+      d->pd == 1 && d->ph == 1 && d->pw == 1 && d->od == d->d && d->oh == d->h && d->ow == d->w) {
+    const long long cols = (long long)d->n * d->h * d->w * (d->c / 8);  // one thread walks the frames
+    const int nb = (int)((cols + 255) / 256);
+    if (d->dtype == FAC_DTYPE_BF16)
+      maxpool3_s1<BF16><<<nb, 256, 0, st>>>(*d, (int)cols);
+    else
+      maxpool3_s1<F16><<<nb, 256, 0, st>>>(*d, (int)cols);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  const int nb = (int)((total + 255) / 256);
   if (d->dtype == FAC_DTYPE_BF16)
     pool_nd<BF16><<<nb, 256, 0, st>>>(*d, (int)total);
   else

@@ -10,6 +10,7 @@ every call goes through ``libfac_cvit.so`` and raises if it cannot.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -264,6 +265,8 @@ def max_pool_sep(x: torch.Tensor, kernel, stride, padding=0) -> torch.Tensor:
     each output reads kw + kh + kd inputs instead of kw * kh * kd (27 -> 9
     for S3D's 3x3x3 pools) and the strided axes shrink the later passes."""
     k, s, p = _triple(kernel), _triple(stride), _pads(padding)
+    if k == (3, 3, 3) and s == (1, 1, 1) and p == (1, 1, 1) and os.environ.get("FAC_POOL_MAX3", "1") != "0":
+        return pool(x, kernel, stride, padding, "max")  # fac_pool_nd's one-pass sliding-window kernel
     y = x
     for ax in (2, 1, 0):
         if k[ax] == 1 and s[ax] == 1 and p[ax] == 0:

@@ -161,6 +161,25 @@ def test_pool_nd(dt):
     assert _ulps(ya.cpu(), ra.to(T16[dt]), dt).max() <= 1.0
 
 
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("d", [1, 2, 5])
+def test_max_pool_3x3x3_s1(dt, d):
+    """The one-pass sliding-window kernel for MaxPool3d(3, 1, 1) (S3D's
+    Inception branch3): bit-exact vs torch, also into a channel slot."""
+    from fac_fake_amd.ops import max_pool_sep, pool
+    g = torch.Generator().manual_seed(5 + d)
+    x = torch.randn(3, 40, d, 9, 13, generator=g).to(T16[dt])
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV)
+    y = max_pool_sep(xg, 3, 1, 1)
+    big = torch.zeros(3, d, 9, 13, 64, dtype=T16[dt], device=DEV)
+    pool(xg, 3, 1, 1, "max", out=big, c_off=16)
+    torch.cuda.synchronize()
+    r = F.max_pool3d(x.float(), 3, 1, 1).permute(0, 2, 3, 4, 1)
+    assert torch.equal(y.cpu().float(), r)
+    bc = big.cpu().float()
+    assert torch.equal(bc[..., 16:56], r) and bc[..., :16].abs().max() == 0 and bc[..., 56:].abs().max() == 0
+
+
 def test_kan_linear_vs_reference(golden):
     from fac_fake_amd.ops import KANLinearLayer
     g = golden("resvitkan_golden.npz")
