@@ -705,10 +705,10 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
 }
 
 
-// ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128} — ResNet-50's
+// ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128, 256} — ResNet-50's
 // bottleneck expansions (conv3 64 -> 256 / 128 -> 512 + residual + ReLU,
 // ResVitKan.py:187's torchvision resnet50 layer1/layer2), their downsample
-// 1x1s and layer1's 64 -> 64 reductions.  Through the generic implicit GEMM
+// 1x1s, layer1's 64 -> 64 reductions and the K = 256 reductions / layer3 expansions.  Through the generic implicit GEMM
 // these are HBM-bound with one or two K steps per 128-row tile, so every
 // workgroup is a serial load -> MFMA -> LDS-staged store chain and the chip
 // holds too few bytes in flight.  Here a persistent workgroup keeps its
@@ -1068,13 +1068,18 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
                                            (uint16_t*)d->out, nbox, d->h, d->w, d->oh, d->ow, k_pad, relu_on);
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
-  // stride-1 1x1 convs with K = cin in {64, 128}: conv_pw
+  // stride-1 1x1 convs with K = cin in {64, 128, 256}: conv_pw
   static const bool pw_on = [] {
     const char* e = std::getenv("FAC_CONV_PW");
     return !(e && e[0] == '0');
   }();
+  static const bool pw256 = [] {
+    const char* e = std::getenv("FAC_PW_K256");
+    return !(e && e[0] == '0');
+  }();
   if (pw_on && !split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
-      d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->cin == 64 || d->cin == 128) && k_pad == d->cin &&
+      d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->cin == 64 || d->cin == 128 || (d->cin == 256 && pw256)) &&
+      k_pad == d->cin &&
       d->cout % 64 == 0 && d->ldo % 4 == 0 && d->c_off % 4 == 0 && !(d->flags & FAC_CONV_OUT_F32) &&
       (!(d->flags & FAC_CONV_RESID) || (d->ldr % 8 == 0 && d->r_off % 8 == 0))) {
     int dev = 0, ncu = 256;
@@ -1102,10 +1107,12 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
   conv_pw<TT, KC, RT, R><<<grid, 256, 0, st>>>(in, wt, d->bias, res, o, mi, k_pad, d->ldo, d->c_off, d->ldr, d->r_off, d->flags)
     if (d->dtype == FAC_DTYPE_BF16) {
       if (d->cin == 64) r ? FAC_PW(BF16, 2, 2, true) : FAC_PW(BF16, 2, 2, false);
-      else r ? FAC_PW(BF16, 4, 1, true) : FAC_PW(BF16, 4, 1, false);
+      else if (d->cin == 128) r ? FAC_PW(BF16, 4, 1, true) : FAC_PW(BF16, 4, 1, false);
+      else r ? FAC_PW(BF16, 8, 1, true) : FAC_PW(BF16, 8, 1, false);
     } else {
       if (d->cin == 64) r ? FAC_PW(F16, 2, 2, true) : FAC_PW(F16, 2, 2, false);
-      else r ? FAC_PW(F16, 4, 1, true) : FAC_PW(F16, 4, 1, false);
+      else if (d->cin == 128) r ? FAC_PW(F16, 4, 1, true) : FAC_PW(F16, 4, 1, false);
+      else r ? FAC_PW(F16, 8, 1, true) : FAC_PW(F16, 8, 1, false);
     }
 #undef FAC_PW
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;

@@ -60,9 +60,10 @@ CONV_CASES = [
     # the space-to-depth first conv (ops.hip conv_s2d4: 4x4/1, 16 -> 64, 8 x 28 boxes)
     (2, 2, 19, 31, 16, 64, (1, 4, 4), 1, 0),
     (1, 1, 59, 59, 16, 64, (1, 4, 4), 1, 0),
-    # stride-1 1x1 convs with cin 64 / 128 (ops.hip conv_pw; case 0 too)
+    # stride-1 1x1 convs with cin 64 / 128 / 256 (ops.hip conv_pw; case 0 too)
     (3, 1, 23, 29, 128, 192, (1, 1, 1), 1, 0),
     (1, 1, 56, 56, 64, 256, (1, 1, 1), 1, 0),
+    (2, 1, 14, 15, 256, 128, (1, 1, 1), 1, 0),
 ]
 
 
@@ -88,7 +89,7 @@ def test_conv_nd_vs_torch_fp32(case, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
-@pytest.mark.parametrize("cin,cout", [(64, 256), (128, 512)])
+@pytest.mark.parametrize("cin,cout", [(64, 256), (128, 512), (256, 1024), (256, 64)])
 def test_conv_pw_residual_into_slot(cin, cout, dt):
     """conv_pw's bottleneck epilogue relu(relu(conv + b) + res) written into
     a channel slot of a wider buffer, over enough positions (40 000, ragged
