@@ -708,8 +708,9 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
 // ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128, 256} — ResNet-50's
 // bottleneck expansions (conv3 64 -> 256 / 128 -> 512 + residual + ReLU,
 // ResVitKan.py:187's torchvision resnet50 layer1/layer2), their downsample
-// 1x1s, layer1's 64 -> 64 reductions and the K = 256 reductions / layer3 expansions.  Through the generic implicit GEMM
-// these are HBM-bound with one or two K steps per 128-row tile, so every
+// 1x1s, layer1's 64 -> 64 reductions, the K = 256 reductions and layer3's
+// 256 -> 1024 expansions.  Through the generic implicit GEMM these are
+// HBM-bound with one to four K steps per tile, so every
 // workgroup is a serial load -> MFMA -> LDS-staged store chain and the chip
 // holds too few bytes in flight.  Here a persistent workgroup keeps its
 // 64-column weight block in LDS and walks row tiles of 64 * RT positions:
