@@ -865,7 +865,7 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
   const int SLAB = D * 16 * Cin;                          // elements per slab buffer
   uint16_t* const wts = smem;
   uint16_t* const slab0 = smem + KS * 2048;
-  const int units_per_clip = S >> 4;
+  const int units_per_clip = (S + 15) >> 4;  // the last unit of a clip may be partial
 
   auto issue_slab = [&](uint16_t* dst, int u) {
     const int n = u / units_per_clip, p0 = (u - n * units_per_clip) << 4;
@@ -875,7 +875,7 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
       const int dp = sl / NP, j = sl - dp * NP;     // dp = d * 16 + p
       const int d = dp >> 4, p = dp & 15;
       const uint16_t* src = g_zero16;
-      if (d < D) src = in + (((size_t)n * D + d) * S + p0 + p) * Cin + ((j ^ (p & 7)) << 3);
+      if (d < D && p0 + p < S) src = in + (((size_t)n * D + d) * S + p0 + p) * Cin + ((j ^ (p & 7)) << 3);
       glds16(src, dst + b * 8);
     }
   };
@@ -919,7 +919,7 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
       const int n = u / units_per_clip, p0 = (u - n * units_per_clip) << 4;
       uint16_t* o = out + (((size_t)n * 8 + z) * S + p0 + r16) * ldo + c_off + nb * 64 + 4 * g;
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = 0; ct < 4 && p0 + r16 < S; ++ct) {
         f32x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = relu_on ? relu(acc[ct][j] + bv[ct][j]) : acc[ct][j] + bv[ct][j];
@@ -1118,10 +1118,15 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
 #undef FAC_PW
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
-  // S3D's temporal (kd,1,1) convs with 8 output frames over 16-aligned
-  // spatial maps: conv_tk (LDS slab per 16 positions, weights resident)
+  static const bool tk_ragged = [] {
+    const char* e = std::getenv("FAC_TK_RAGGED");
+    return !(e && e[0] == '0');
+  }();
+  // S3D's temporal (kd,1,1) convs with 8 output frames: conv_tk (LDS slab per
+  // 16 positions, the last one of a clip partial when 16 does not divide h*w)
   if (!split && d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 && d->pw == 0 && d->od == 8 &&
-      d->cin % 64 == 0 && d->cout % 64 == 0 && (d->h * d->w) % 16 == 0 && d->ldo % 4 == 0 && d->c_off % 4 == 0 &&
+      d->cin % 64 == 0 && d->cout % 64 == 0 && (tk_ragged || (d->h * d->w) % 16 == 0) && d->ldo % 4 == 0 &&
+      d->c_off % 4 == 0 &&
       (d->flags & ~FAC_CONV_RELU) == 0 && k_pad == d->kd * d->cin) {
     const int ks = d->kd * d->cin / 32, slab = d->d * 16 * d->cin;
     const int db = ks * 2048 + 2 * slab <= 81920 ? 2 : (ks * 2048 + slab <= 81920 ? 1 : 0);
@@ -1130,7 +1135,7 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
       if (hipGetDevice(&dev) != hipSuccess ||
           hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
         ncu = 256;
-      const int nunits = d->n * (d->h * d->w / 16);
+      const int nunits = d->n * ((d->h * d->w + 15) / 16);
       const dim3 grid(std::min(nunits, ncu), d->cout / 64);
       const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
       if (d->dtype == FAC_DTYPE_BF16)

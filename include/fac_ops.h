@@ -49,7 +49,7 @@ extern "C" {
  * Shapes with a dedicated kernel are routed to it inside this call (same
  * contract): the 4x4/1 16->64 conv over space-to-depth cells (conv_s2d4:
  * ResNet-50's / S3D's first conv) and temporal (kd,1,1) convs with 8 output
- * frames over 16-aligned maps, cin % 64 == 0, cout % 64 == 0 (conv_tk), and
+ * frames, cin % 64 == 0, cout % 64 == 0 (conv_tk), and
  * stride-1 1x1 convs with cin 64, 128 or 256, cout % 64 == 0, no fp32
  * output (conv_pw: ResNet-50's K <= 256 bottleneck 1x1s).  FAC_CONV_PW=0 in the
  * environment keeps the latter on the generic kernel. */

@@ -57,6 +57,8 @@ CONV_CASES = [
     # S3D's temporal convs with 8 output frames (ops.hip conv_tk)
     (2, 16, 8, 8, 64, 64, (7, 1, 1), (2, 1, 1), (3, 0, 0)),
     (2, 8, 4, 8, 192, 192, (3, 1, 1), 1, (1, 0, 0)),
+    (2, 8, 7, 9, 64, 128, (3, 1, 1), 1, (1, 0, 0)),           # 63 positions: partial last unit
+    (1, 16, 14, 14, 192, 64, (7, 1, 1), (2, 1, 1), (3, 0, 0)),  # 196 positions
     # the space-to-depth first conv (ops.hip conv_s2d4: 4x4/1, 16 -> 64, 8 x 28 boxes)
     (2, 2, 19, 31, 16, 64, (1, 4, 4), 1, 0),
     (1, 1, 59, 59, 16, 64, (1, 4, 4), 1, 0),
