@@ -56,14 +56,18 @@ def _check_conv_waits(compile_fn, verbose: bool) -> None:
     if verbose:
         print(f"isa_check: {rep.kernels} conv kernels, {rep.waits} relaxed LDS waits, "
               f"{len(rep.problems)} problems", file=sys.stderr)
-    if rep.ok:
+    if rep.ok and rep.kernels > 0:
         return
+    if rep.kernels == 0:
+        # nothing disassembled (bundle name mismatch, no llvm-objdump): the
+        # relaxed waits cannot be verified, so build the strict variant
+        rep.problems.append("no conv3x3 kernels found in the disassembly; relaxed waits unverified")
     print("isa_check: relaxed LDS waits unsound in this build, rebuilding conv.hip with "
           "FAC_CONV_STRICT_LGKM:\n  " + "\n  ".join(rep.problems[:8]), file=sys.stderr)
     FILE_FLAGS["conv.hip"] = FILE_FLAGS.get("conv.hip", []) + ["-DFAC_CONV_STRICT_LGKM"]
     compile_fn((CSRC / "conv.hip", obj))
     rep = isa_check.check_objects([obj], arch=ARCH)
-    if not rep.ok:
+    if not rep.ok:  # (zero kernels found is fine here: every wait is strict)
         raise RuntimeError("isa_check failed even with strict LDS waits:\n" + "\n".join(rep.problems[:8]))
 
 

@@ -131,7 +131,11 @@ struct fac_ctx {
            *o = nullptr, *hbuf = nullptr, *cbuf = nullptr;
   int cap_chunk = 0;  // crops act0/act1 hold
   float *slab = nullptr, *x = nullptr, *qkv = nullptr, *hh = nullptr;
-  int* errflag = nullptr;
+  // pos_index range flag: host-visible pinned memory (hipHostMalloc, mapped),
+  // written by embed_finalize_ln with a plain system-scope store, read by the
+  // host at the start of the next forward without a device sync
+  int* errflag = nullptr;      // device view
+  int* err_host = nullptr;     // host view of the same int
   int* sched = nullptr;  // 2 ints: stem224 dynamic box counter + finished-workgroup count
   int stem_dynamic = 1;  // option "stem_dynamic": stem224 claims boxes from `sched` (else static)
   int stem_nwg = 0;      // option "stem_nwg": persistent stem workgroups (0 = one per CU)
@@ -156,6 +160,17 @@ namespace {
 int set_err(fac_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
+}
+
+// FAC_ERR_ARG if an earlier forward of this context saw a pos_index outside
+// [0,32) (the device clamps it and raises the flag; the flag is read here,
+// on the host, at the next call — no synchronisation)
+int take_device_error(fac_ctx* c) {
+  if (c && c->err_host && *(volatile int*)c->err_host) {
+    *(volatile int*)c->err_host = 0;
+    return set_err(c, FAC_ERR_ARG, "a previous forward had a pos_index outside [0,32) (clamped on the device)");
+  }
+  return 0;
 }
 
 #define HIP_TRY(ctx, expr)                                                                  \
@@ -247,7 +262,15 @@ int ensure_ws(fac_ctx* c, int B) {
   c->hbuf = (uint16_t*)(base + L.hbuf);
   c->cbuf = (uint16_t*)(base + L.cbuf);
   c->hh = (float*)(base + L.hh);
-  c->errflag = (int*)(base + L.err);
+  if (!c->err_host) {
+    void* hp = nullptr;
+    HIP_TRY(c, hipHostMalloc(&hp, 256, hipHostMallocMapped | hipHostMallocCoherent));
+    c->err_host = (int*)hp;
+    *(volatile int*)c->err_host = 0;
+    void* dp = nullptr;
+    HIP_TRY(c, hipHostGetDevicePointer(&dp, hp, 0));
+    c->errflag = (int*)dp;
+  }
   c->sched = (int*)(base + L.sched);  // stem224 box counters (zeroed above, self-resetting)
   c->zero16 = (uint16_t*)(base + L.zero);  // the whole workspace was just zeroed
   c->ws_bytes = L.total;
@@ -437,6 +460,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
     return set_err(c, FAC_ERR_NOT_LOADED, "tail-only context has no conv stem: use fac_forward_features");
   if (B <= 0 || (!in && !stem_in) || (stop_after < 0 && !conv_only && (!pidx || !logits)))
     return set_err(c, FAC_ERR_ARG, "bad forward arguments");
+  if (int e = take_device_error(c)) return e;
   DevGuard g(c->device);
   int rc = ensure_ws(c, B);
   if (rc) return rc;
@@ -737,6 +761,7 @@ int fac_forward_features(fac_ctx* c, const void* d_feat, int B, const int32_t* d
   if (!d_feat || !d_pos || B <= 0 || (!d_hidden && !d_logits))
     return set_err(c, FAC_ERR_ARG, "bad fac_forward_features arguments");
   if (B > 32 * 1024) return set_err(c, FAC_ERR_SHAPE, "batch too large");
+  if (int e = take_device_error(c)) return e;
   DevGuard g(c->device);
   int rc = ensure_ws(c, B);
   if (rc) return rc;
@@ -878,11 +903,11 @@ int fac_stem_event_ms(fac_ctx* c, float* avg_ms, int* n_launches) {
 int fac_check_device_errors(fac_ctx* c, int* flags) {
   if (!c || !flags) return FAC_ERR_ARG;
   *flags = 0;
-  if (!c->errflag) return FAC_OK;
+  if (!c->err_host) return FAC_OK;
   DevGuard g(c->device);
   HIP_TRY(c, hipDeviceSynchronize());
-  HIP_TRY(c, hipMemcpy(flags, c->errflag, sizeof(int), hipMemcpyDeviceToHost));
-  HIP_TRY(c, hipMemset(c->errflag, 0, sizeof(int)));
+  *flags = *(volatile int*)c->err_host;
+  *(volatile int*)c->err_host = 0;
   return FAC_OK;
 }
 
@@ -909,6 +934,7 @@ void fac_destroy(fac_ctx* c) {
     if (c->ev_stack) (void)hipEventDestroy(c->ev_stack);
     for (void* p : c->weights) (void)hipFree(p);
     if (c->ws) (void)hipFree(c->ws);
+    if (c->err_host) (void)hipHostFree(c->err_host);
   }
   delete c;
 }

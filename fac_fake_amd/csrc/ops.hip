@@ -651,7 +651,7 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bv[ct][j] = bias[(2 * wn + ct) * 16 + 4 * g + j];
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[(2 * wn + ct) * 16 + 4 * g + j] : 0.f;
   // this lane's halo slot offsets (16-byte units) for pixel tile i at tap (0, g/2)
   int bo[7];
 #pragma unroll
@@ -892,12 +892,15 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bv[ct][j] = bias[nb * 64 + ct * 16 + 4 * g + j];
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[nb * 64 + ct * 16 + 4 * g + j] : 0.f;
   const int z = wave;  // output frame of this wave (Do == 8)
   for (int it = 0; u < nunits; ++it) {
     const int next = u + gridDim.x;
     uint16_t* const cur = slab0 + (db == 2 ? (it & 1) * SLAB : 0);
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // slab u in; the other buffer's readers done
+    // slab u in; the other buffer's readers done.  lgkmcnt(0) too: the weight
+    // block above was written with plain ds_writes, which must have landed
+    // before any other wave reads it (first iteration)
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (db == 2 && next < nunits) issue_slab(slab0 + ((it + 1) & 1) * SLAB, next);
     f32x4 acc[4];
 #pragma unroll

@@ -205,7 +205,7 @@ __global__ __launch_bounds__(64) void embed_finalize_ln(const float* __restrict_
   const int r = blockIdx.x, b = r >> 1, lane = threadIdx.x;
   int p = pidx[b];
   if (p < 0 || p >= 32) {
-    if (lane == 0 && (r & 1) == 0) atomicOr(err, 1);
+    if (lane == 0 && (r & 1) == 0 && err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     p = p < 0 ? 0 : 31;
   }
   f32x4 v[4];

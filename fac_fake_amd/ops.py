@@ -54,6 +54,8 @@ def _zero256(device: torch.device) -> torch.Tensor:
     """256 zero bytes of device memory: the source of conv.hip's zero-padding loads."""
     key = (device.type, device.index)
     if key not in _ZERO256:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("the zero page must be allocated before graph capture (construct the layers first)")
         _ZERO256[key] = torch.zeros(128, dtype=torch.int16, device=device)
     return _ZERO256[key]
 
@@ -146,10 +148,20 @@ class ConvLayer:
             self._w33 = w[:, :, 0].reshape(co, ci, 9).contiguous()
             self._pk33 = {}
             self._device = device
+            _zero256(torch.device(device))  # allocated (and zeroed) before any graph capture
+            # packed now for every resolution conv.hip has tiles for, so a
+            # forward never packs (a synchronous host->device copy) inside a
+            # graph capture
+            for h in (112, 56, 28, 14, 7):
+                self._packed33(h)
 
     def _packed33(self, h: int):
         """fac_conv3x3 weights for h x h inputs, or None if conv.hip has no tile for it."""
         if h not in self._pk33:
+            if torch.cuda.is_current_stream_capturing():
+                # packing copies host -> device synchronously: illegal inside a capture
+                raise RuntimeError(f"conv weights for {h}x{h} inputs are packed on first use: run one eager "
+                                   "forward (or the model's reserve()) at this input size before graph capture")
             lib = _lib.load()
             n = lib.fac_conv3x3_packed_elems(h, self.cin, self.cout)
             pk = None

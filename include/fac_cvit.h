@@ -143,8 +143,14 @@ int fac_profile_forward_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32
  * taken over its timed region with this. */
 int fac_stem_event_ms(fac_ctx* ctx, float* avg_ms, int* n_launches);
 
-/* Nonzero if a previous forward saw a pos_index outside [0,32) (clamped).
- * Synchronises the context's device; not for use inside graph capture. */
+/* pos_index outside [0,32): the device clamps it (the kernel cannot return
+ * an error) and raises a host-visible flag; the context's NEXT forward call
+ * (fac_forward_*, fac_forward_features, pipelined) then returns FAC_ERR_ARG
+ * before enqueueing anything and clears the flag.  fac_check_device_errors
+ * reads (and clears) the flag after synchronising the device: nonzero if a
+ * forward since the last check saw such an index.  Not for use inside graph
+ * capture (a captured forward's flag is seen by the first eager call after
+ * the replay completes). */
 int fac_check_device_errors(fac_ctx* ctx, int* flags);
 
 /* Video-level score over n logit pairs (pred_sig + pre_process_prediction,

@@ -42,7 +42,8 @@ extern "C" {
  * weight: 16-bit [cout_pad][k_pad], row o = output channel, k index =
  *   ((tz*kh + ty)*kw + tx)*cin + c, zero beyond taps*cin; cout_pad a
  *   multiple of 128, k_pad a multiple of 64 (fac_conv_weight_layout).
- * bias: fp32 [cout_pad] (BN shift folded in).
+ * bias: fp32 [cout_pad] (BN shift folded in), or NULL for none (every
+ *   routed kernel honours NULL).
  * out: row m = ((n*Do + z)*Ho + y)*Wo + x, element [m*ldo + c_off + c];
  *   c_off lets Inception branches write straight into their concat slot.
  * residual (FAC_CONV_RESID): 16-bit [m*ldr + r_off + c].

@@ -38,12 +38,17 @@ def golden():
     return _load
 
 
-@pytest.fixture(scope="session")
+@pytest.fixture(scope="session", autouse=True)
 def built_lib():
-    """Build libfac_cvit.so if it is missing (hipcc cross-compiles without a GPU)."""
+    """(Re)build libfac_cvit.so when any source is newer than it (mtime-checked,
+    hipcc cross-compiles without a GPU), so a stale shipped .so is never what
+    gets tested.  On a box without hipcc the shipped library is used as is."""
     from fac_fake_amd import build
-    if not build.LIB.exists():
+    try:
         build.build()
+    except RuntimeError as e:
+        if not build.LIB.exists() or "hipcc not found" not in str(e):
+            raise
     return build.LIB
 
 

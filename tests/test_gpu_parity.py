@@ -266,6 +266,34 @@ def test_reference_forward_contract(models):
     assert out.shape == (2, 2) and out.dtype == torch.float32
 
 
+def test_out_of_range_pos_index_is_an_error_at_the_c_abi(models):
+    """SURVEY §8b error convention: a pos_index outside [0,32) cannot be
+    reported by the kernel that reads it, so the device clamps it and raises
+    a host-visible flag; the context's next forward returns FAC_ERR_ARG (and
+    enqueues nothing), and fac_check_device_errors reports it after a sync."""
+    import ctypes
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models["fp16"]
+    ctx = m._ctx
+    x = torch.from_numpy(make_crops(4, seed=19)).to(DEV)
+    lg = torch.empty(4, 2, device=DEV)
+    good = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device=DEV)
+    bad = torch.tensor([0, 1, 40, 3], dtype=torch.int32, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
+    torch.cuda.synchronize()
+    rc = lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st)
+    assert rc == -1 and b"pos_index" in lib.fac_last_error(ctx)
+    assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0  # cleared
+    assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
+    flags = ctypes.c_int()
+    assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == 1
+    assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == 0
+    assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0
+    torch.cuda.synchronize()
+
+
 def test_chunked_video_prediction(models, golden):
     """predict()'s chunking on 40 crops ([0:32] then [32:40]) and the video score."""
     from fac_fake_amd.prediction import predict_crops
