@@ -65,18 +65,68 @@ def pmc_traffic(stage: str, dtype: str):
     return (t["hbm_bytes"] if t else None), files[-1].name
 
 
-def cpu_baseline(sd, threads: int, iters: int = 4, batch: int = 32):
+def pmc_mfma_busy(stage: str, dtype: str):
+    """MFMA utilisation of `stage`'s kernel from the newest committed PMC
+    summary (profiles/*_{dtype}_pmc.json, tools/pmc_summary.py):
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x CUs) per launch, or None."""
+    files = sorted((REPO / "profiles").glob(f"*_{dtype}_pmc.json"))
+    if not files:
+        return None, None
+    try:
+        t = json.loads(files[-1].read_text()).get("by_stage", {}).get(stage)
+    except (OSError, ValueError):
+        return None, None
+    return (t.get("mfma_busy") if t else None), files[-1].name
+
+
+def host_cpu_info() -> dict:
+    """Host CPUs this process may use: the affinity mask, capped by a cgroup
+    CPU quota when one is set (the GPU box shares its host: os.cpu_count()
+    reports the whole machine, the job's share is smaller)."""
+    n_host = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = n_host
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"os_cpu_count": n_host, "affinity": usable, "cgroup_quota_cpus": quota,
+            "usable": min(usable, quota) if quota else usable, "model": model}
+
+
+def cpu_baseline(sd, threads: int, info: dict, warmup: int = 3, iters: int = 5, batch: int = 32):
+    """The reference forward's PyTorch CPU kernels (oracle.cvit_torch.forward_fp32,
+    checked bit-equal to CViT-main/model/cvit.py by tests/test_oracle.py) on
+    B=32 crops (the reference's largest chunk), fp32, `threads` intra-op
+    threads, `warmup` untimed + `iters` timed passes."""
     from oracle.cvit_torch import forward_fp32, normalize_u8
     torch.set_num_threads(threads)
     x = normalize_u8(make_crops(batch, seed=2))
-    forward_fp32(sd, x)  # warm-up
+    for _ in range(warmup):
+        forward_fp32(sd, x)
     t0 = time.perf_counter()
     for _ in range(iters):
         forward_fp32(sd, x)
     dt = time.perf_counter() - t0
     return {"value": round(iters * batch / dt, 3), "unit": "face-crops/s", "cores": threads, "kind": "port",
-            "sample": f"{iters} x {batch} crops (fp32 PyTorch CPU restatement of cvit.py forward, "
-                      f"1 warm-up), torch {torch.__version__}"}
+            "sample": f"{iters} timed x {batch} crops after {warmup} warm-up passes (fp32 PyTorch CPU restatement "
+                      f"of cvit.py forward), {threads} threads = every CPU this job may use "
+                      f"(os.cpu_count() {info['os_cpu_count']}, affinity {info['affinity']}, cgroup quota "
+                      f"{info['cgroup_quota_cpus']}); CPU: {info['model']}; torch {torch.__version__}",
+            "host": info}
 
 
 def video_measurement(model, dev, world: int, n_frames: int = 300, reps: int = 3):
@@ -91,7 +141,9 @@ def video_measurement(model, dev, world: int, n_frames: int = 300, reps: int = 3
     from fac_fake_amd import video
     frames, boxes = video.synthetic_video(n_frames, 1080, 1920, seed=3, device=dev)
     out = {"workload": f"config 3: {n_frames}-frame 1080x1920 synthetic video, 1 box/frame, crop+resize+CViT+score",
-           "n_gpus": world}
+           "n_gpus": world,
+           "boxes": f"square, {video.BOX_MIN}..{video.BOX_MIN + video.BOX_SPAN - 1} px, splitmix64 seed 3 (boxes under "
+                    "224 px take INTER_AREA's upscale branch; rounds 1-2 up to a82f6ac used 240..559 px)"}
     for mode in ("dense", "reference"):
         video.predict_video(model, frames, boxes, mode=mode)  # warm-up
         torch.cuda.synchronize(dev)
@@ -340,6 +392,7 @@ def main():
                          "that overlaps batch k's encoder with batch k+1's conv stack")
     ap.add_argument("--no-fuse", action="store_true", help="unfused conv1..conv3 (A/B of the fused 224 block)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp16-line", action="store_true", help="skip the same measurement in the other 16-bit dtype")
     ap.add_argument("--no-video", action="store_true", help="skip the config-3 video sub-measurement")
     ap.add_argument("--no-resvitkan", action="store_true", help="skip the config-5 ResVitKan sub-measurement")
     ap.add_argument("--no-s3d", action="store_true", help="skip the config-4 S3D sub-measurement")
@@ -375,10 +428,98 @@ def main():
             print(json.dumps(r), flush=True)
         return
 
-    lib = _lib.load()
     sd = make_state_dict(0)
+    headline = cvit_measurement(args, args.dtype, dev, world, rank, sd, keep_model=not args.no_video)
+    r = headline
+    value = r["value"]
+    peak = PEAK_TFLOPS[args.dtype]
+    line = {
+        "metric": "face-crops/sec at 224x224 bf16, CViT forward, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "face-crops/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic uint8 224x224 crops (splitmix64), deterministic synthetic CViT weights (no trained "
+                "checkpoint in the reference)",
+        "config": {"workload": "config 2: CViT forward, B=256 crops per GPU per step, pos slot j mod 32",
+                   "model": "CViT(224,7,2,512,1024,6,8,2048)", "global_batch": world * B, "seq_len": 2,
+                   "parallelism": f"frame-sharded x{world}" + (" + RCCL logit all-gather" if world > 1 else ""),
+                   "graph": r["graph"], "stem_chunk": args.stem_chunk,
+                   "fused_stem224": not args.no_fuse, "pipelined": r["pipelined"],
+                   **({"options": args.opt} if args.opt else {})},
+        "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
+        "parity": r["parity"],
+        "roofline": r["roofline"],
+        "stage_ms": r["stage_ms"],
+    }
+    # the same measurement in fp16 (same MFMA rate on gfx950): the dtype that
+    # meets the north star's 1e-3 per-frame bar
+    if not args.no_fp16_line:
+        other = "fp16" if args.dtype == "bf16" else "bf16"
+        o = cvit_measurement(args, other, dev, world, rank, sd, keep_model=False)
+        line[other] = {"value": round(o["value"], 2), "unit": "face-crops/s",
+                       "ms_per_step": round(o["elapsed"] / args.steps * 1e3, 4), "parity": o["parity"],
+                       "mfma_roofline_fraction": round(o["value"] * FLOP_PER_CROP / (world * peak * 1e12), 4),
+                       "roofline_frac": o["roofline"]["frac"], "stem_launch_ms": o["roofline"]["launch_ms"]}
+    model = headline.pop("model", None)
+    if not args.no_video and model is not None:
+        line["config3"] = video_measurement(model, dev, world)
+    # The sub-measurements below are independent workloads: release this
+    # context first.  Its high-priority tail stream (the software pipeline)
+    # otherwise stays mapped to one of the process's hardware queues
+    # (GPU_MAX_HW_QUEUES, 4), and the S3D graph's parallel branch streams
+    # then share queues: measured 20.5k vs 27.2k clips/s for the same graph.
+    torch.cuda.synchronize(dev)
+    if model is not None:
+        model._release()
+        del model
+    if not args.no_s3d:
+        line["config4"] = s3d_measurement(dev, args.dtype, world)
+    if not args.no_resvitkan:
+        line["config5"] = resvitkan_measurement(dev, args.dtype, world)
+    if not args.no_repbn8:
+        line["variant_repbn8"] = repbn8_measurement(dev, args.dtype, world)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        info = host_cpu_info()
+        threads = args.cpu_threads or info["usable"]
+        line["cpu_baseline"] = cpu_baseline(sd, threads, info)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def parity_vs_golden(logits: torch.Tensor, B: int, rank: int):
+    """max|dp| of the per-logit sigmoid of the timed batch's logits against
+    tests/golden/golden_b256.npz (fp32 outputs of the reference module on the
+    same seed-3 crops and slots, tools/make_golden.py): a data fixture, not the
+    oracle.  Only rank 0 scores the golden crops (other ranks use other seeds)."""
+    g = REPO / "tests" / "golden" / "golden_b256.npz"
+    if rank != 0 or B != 256 or not g.exists():
+        return None
+    ref = np.load(g, allow_pickle=False)["logits"].astype(np.float64)
+    got = logits.detach().float().cpu().numpy().astype(np.float64)
+    sig = lambda x: 1.0 / (1.0 + np.exp(-x))  # noqa: E731
+    dp = float(np.abs(sig(got) - sig(ref)).max())
+    return {"max_abs_dprob": round(dp, 7), "vs": "tests/golden/golden_b256.npz (reference cvit.py, fp32)",
+            "bar": 1e-3, "meets_bar": dp <= 1e-3}
+
+
+def cvit_measurement(args, dtype: str, dev, world: int, rank: int, sd, keep_model: bool):
+    """Config 2 (BASELINE.json configs[1]) at `dtype`: K timed steps of the
+    CViT forward over B=256 HBM-resident crops (after W warm-up steps),
+    pipelined by default; returns throughput, the dominant kernel's roofline,
+    per-stage times and the parity of the last timed batch."""
+    lib = _lib.load()
     from fac_fake_amd.cvit import CViT
-    model = CViT(dtype=args.dtype)
+    B = args.batch
+    model = CViT(dtype=dtype)
     model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     model.to(dev)
     model.reserve(B, dev)
@@ -421,6 +562,11 @@ def main():
 
     kstep = [0]
 
+    def gather_score(lg):
+        dist.all_gather_into_tensor(gathered, lg)
+        _lib.check(lib.fac_video_score(gathered.data_ptr(), world * B, score.data_ptr(), stream.cuda_stream),
+                   None, "video_score")
+
     def step_pipelined():
         # batch k: conv stack on `stream`, encoder + head (+ score at N=1) on the
         # context's tail stream; at N>1 the logits of batch k-1 are gathered
@@ -436,11 +582,6 @@ def main():
             if world > 1 and k > 0:
                 _lib.check(lib.fac_pipeline_join(ctx, 1, stream.cuda_stream), ctx, "join")
                 gather_score(logits_pp[(k - 1) & 1])
-
-    def gather_score(lg):
-        dist.all_gather_into_tensor(gathered, lg)
-        _lib.check(lib.fac_video_score(gathered.data_ptr(), world * B, score.data_ptr(), stream.cuda_stream),
-                   None, "video_score")
 
     def drain():
         # every enqueued batch complete (and, at N>1, the last one gathered + scored)
@@ -488,6 +629,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    last_logits = logits_pp[(args.steps - 1) & 1] if pipelined else logits
+    parity = parity_vs_golden(last_logits, B, rank)
     stem_ms_timed, stem_n = None, 0
     if stem_events:
         avg, cnt = ctypes.c_float(), ctypes.c_int()
@@ -524,60 +667,27 @@ def main():
         launch_ms = stem_ms_timed
         launch_src = f"mean of the {stem_n} launches in the timed region (hipEvents on the launching stream)"
     achieved = dom_flops / (launch_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(STAGE_NAMES[dom], args.dtype)
-    peak = PEAK_TFLOPS[args.dtype]
-
-    value = world * B * args.steps / elapsed
-    line = {
-        "metric": "face-crops/sec at 224x224 bf16, CViT forward, 1/2/4/8 MI355X",
-        "value": round(value, 2),
-        "unit": "face-crops/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": args.dtype,
-        "data": "synthetic uint8 224x224 crops (splitmix64), deterministic synthetic CViT weights (no trained "
-                "checkpoint in the reference)",
-        "config": {"workload": "config 2: CViT forward, B=256 crops per GPU per step, pos slot j mod 32",
-                   "model": "CViT(224,7,2,512,1024,6,8,2048)", "global_batch": world * B, "seq_len": 2,
-                   "parallelism": f"frame-sharded x{world}" + (" + RCCL logit all-gather" if world > 1 else ""),
-                   "graph": graph is not None, "stem_chunk": args.stem_chunk,
-                   "fused_stem224": not args.no_fuse, "pipelined": pipelined, **({"options": args.opt} if args.opt else {})},
-        "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
+    traffic, traffic_src = pmc_traffic(STAGE_NAMES[dom], dtype)
+    mfma_busy, pmc_src = pmc_mfma_busy(STAGE_NAMES[dom], dtype)
+    peak = PEAK_TFLOPS[dtype]
+    out = {
+        "value": world * B * args.steps / elapsed, "elapsed": elapsed, "graph": graph is not None,
+        "pipelined": pipelined, "parity": parity,
         "roofline": {"bound": "mfma", "kernel": dom_name,
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "mfma_busy": mfma_busy, "mfma_busy_source": pmc_src,
                      "launch_ms": round(launch_ms, 4), "launch_ms_source": launch_src,
                      "launch_ms_sync_profile": round(float(conv_ms[dom]), 4), "flops_per_launch": dom_flops},
         "stage_ms": {n: round(float(v), 4) for n, v in zip(STAGE_NAMES, acc)},
     }
-    if not args.no_video:
-        line["config3"] = video_measurement(model, dev, world)
-    # The sub-measurements below are independent workloads: release this
-    # context first.  Its high-priority tail stream (the software pipeline)
-    # otherwise stays mapped to one of the process's hardware queues
-    # (GPU_MAX_HW_QUEUES, 4), and the S3D graph's parallel branch streams
-    # then share queues: measured 20.5k vs 27.2k clips/s for the same graph.
     torch.cuda.synchronize(dev)
-    model._release()
-    del model
-    if not args.no_s3d:
-        line["config4"] = s3d_measurement(dev, args.dtype, world)
-    if not args.no_resvitkan:
-        line["config5"] = resvitkan_measurement(dev, args.dtype, world)
-    if not args.no_repbn8:
-        line["variant_repbn8"] = repbn8_measurement(dev, args.dtype, world)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(sd, threads)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if keep_model:
+        out["model"] = model
+    else:
+        model._release()
+        del model
+    return out
 
 
 if __name__ == "__main__":

@@ -9,7 +9,8 @@ Interface parity with ``CViT-main/model/cvit.py``:
 * ``forward(img, mask=None)`` on normalised fp32 NCHW ``[B,3,224,224]``
   returning fp32 logits ``[B,2]`` (cvit.py:167-179), including the
   reference's batch-slot ``pos_embedding`` rule (crop j of a call gets
-  ``pos_embedding[j]``, cvit.py:174-175) and its ``B > 32`` RuntimeError.
+  ``pos_embedding[j]``, cvit.py:174-175) and its ``B > 32`` RuntimeError;
+  ``mask`` follows the reference's semantics exactly (``reference_mask_poisons``).
 
 The parameters live in a tree of plain containers purely to expose the
 reference's state_dict; the arithmetic never runs through them.  On the first
@@ -42,6 +43,26 @@ SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=
                  mlp_dim=2048)
 MAX_SLOTS = 32  # pos_embedding has 32 rows (cvit.py:154)
 _BUFFER_KINDS = ("rmean", "rvar", "nbt")
+
+
+def reference_mask_poisons(mask, B: int, heads: int = 8, n_tokens: int = 2) -> bool:
+    """The reference's attention mask (cvit.py:50-55; the same code in every
+    CViT variant), evaluated on the host for the [B, heads, 2, 2] score shape:
+    ``F.pad(mask.flatten(1), (1, 0), value=True)``, its outer product, and
+    ``dots.masked_fill_(~mask, -inf)``.  Raises what the reference raises (the
+    AssertionError for a wrong width; the broadcast RuntimeError, since the
+    [B,2,2] mask lines up with dots' [heads,2,2] dims: only B in {1, heads}
+    works).  Returns True when some score is masked: its token's score row
+    is then all -inf, softmax gives NaN, and through ``attn @ v`` (0 * NaN)
+    every crop's logits become NaN (checked against the reference module);
+    False (all positions kept) leaves the forward exactly as with no mask."""
+    m = torch.as_tensor(mask).to("cpu")
+    m = torch.nn.functional.pad(m.flatten(1), (1, 0), value=True)
+    assert m.shape[-1] == n_tokens, "mask has incorrect dimensions"
+    m = m[:, None, :] * m[:, :, None]
+    dots = torch.zeros(B, heads, n_tokens, n_tokens)
+    dots.masked_fill_(~m, float("-inf"))
+    return bool(torch.isinf(dots).any())
 
 
 class _Node(nn.Module):
@@ -212,13 +233,12 @@ class CViT(nn.Module):
         return logits, probs
 
     def forward(self, img: torch.Tensor, mask=None, pos_index=None) -> torch.Tensor:
-        if mask is not None:
-            raise NotImplementedError("mask is not supported by the HIP path (cvit_prediction.py never passes one)")
         if img.dim() != 4 or tuple(img.shape[1:]) != (3, 224, 224):
             raise ValueError(f"expected img [B,3,224,224], got {tuple(img.shape)}")
+        poison = mask is not None and reference_mask_poisons(mask, img.shape[0])
         x = img.to(torch.float32).contiguous()
         logits, _ = self._run(x, x.shape[0], pos_index, u8=False, want_probs=False)
-        return logits
+        return logits.fill_(float("nan")) if poison else logits
 
     def forward_u8(self, crops: torch.Tensor, pos_index=None, return_probs: bool = False):
         """uint8 NHWC RGB face crops [B,224,224,3] -> logits (and per-logit sigmoids)."""

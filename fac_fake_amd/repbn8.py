@@ -38,7 +38,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .cvit import MAX_SLOTS, _Node
+from .cvit import MAX_SLOTS, _Node, reference_mask_poisons
 from .ops import TORCH16, fold_bn, sigmoid
 from .weights import REPBN8_LAYERS, repbn8_param_specs
 
@@ -291,15 +291,15 @@ class CViT(nn.Module):
         return logits, probs
 
     def forward(self, img: torch.Tensor, mask=None, pos_index=None) -> torch.Tensor:
-        if mask is not None:
-            raise NotImplementedError("mask is not supported by the HIP path")
+        poison = mask is not None and reference_mask_poisons(mask, img.shape[0])
         if not img.is_cuda:
             raise RuntimeError("CViT RepBn8 (gfx950 HIP path) needs its input on a GPU device; there is no CPU "
                                "fallback")
         if img.dim() != 4 or tuple(img.shape[1:]) != (3, 224, 224):
             raise ValueError(f"expected img [B,3,224,224], got {tuple(img.shape)}")
         self._prepare(img.device)
-        return self._run(img.float().contiguous(), False, pos_index, False)[0]
+        logits = self._run(img.float().contiguous(), False, pos_index, False)[0]
+        return logits.fill_(float("nan")) if poison else logits
 
     def forward_u8(self, crops: torch.Tensor, pos_index=None, return_probs: bool = False):
         """uint8 NHWC RGB crops [B,224,224,3]; x/255 + Normalize fused into the first conv block."""

@@ -29,7 +29,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .prediction import EMPTY_SCORE, chunk_slots, dense_slots, pre_process_prediction, pred_sig
+from .prediction import EMPTY_SCORE, chunk_slots, dense_slots
 from .sharding import gather_logits, shard_bounds
 from .weights import splitmix64
 
@@ -50,18 +50,24 @@ def frame_indices(length: int) -> list[int]:
     return out
 
 
+BOX_MIN, BOX_SPAN = 112, 448   # synthetic face boxes: square, 112..559 px
+
+
 def synthetic_video(n_frames: int, height: int = 1080, width: int = 1920, seed: int = 3, device=None,
-                    faces_per_frame: int = 1):
+                    faces_per_frame: int = 1, box_min: int = BOX_MIN, box_span: int = BOX_SPAN):
     """Deterministic synthetic video: uint8 BGR frames [F, H, W, 3] on `device`
     (torch's seeded device generator) and face boxes int32 [F*k, 5] =
-    (frame, left, top, right, bottom), square boxes of 112..559 px inside the
-    frame (splitmix64 of `seed`) -- about a quarter of them under 224 px, so
-    both of cv2's INTER_AREA branches (area average / upscale) are exercised."""
+    (frame, left, top, right, bottom), square boxes of box_min..box_min +
+    box_span - 1 px inside the frame (splitmix64 of `seed`).  The default
+    112..559 puts about a quarter of them under 224 px, so both of cv2's
+    INTER_AREA branches (area average / upscale) are exercised; round 1's
+    config-3 numbers used 240..559 (box_min=240, box_span=320), where every
+    crop is an area-average downscale."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device=dev).manual_seed(seed)
     frames = torch.randint(0, 256, (n_frames, height, width, 3), dtype=torch.uint8, device=dev, generator=g)
     r = splitmix64(np.arange(3 * n_frames * faces_per_frame, dtype=np.uint64), seed + 1000).reshape(-1, 3)
-    size = 112 + (r[:, 0] % np.uint64(448)).astype(np.int64)
+    size = box_min + (r[:, 0] % np.uint64(box_span)).astype(np.int64)
     size = np.minimum(size, min(height, width))
     left = (r[:, 1] % (np.uint64(width) - size.astype(np.uint64) + np.uint64(1))).astype(np.int64)
     top = (r[:, 2] % (np.uint64(height) - size.astype(np.uint64) + np.uint64(1))).astype(np.int64)
@@ -136,5 +142,18 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         logits = gather_logits(local.float(), n, group) if world > 1 else local
     else:
         raise ValueError("mode must be 'reference' or 'dense'")
-    score = float(pre_process_prediction(pred_sig(logits.float().cpu())))
+    score = device_video_score(logits)
     return (score, logits) if return_logits else score
+
+
+def device_video_score(logits: torch.Tensor) -> float:
+    """pre_process_prediction(pred_sig(logits)) (cvit_prediction.py:240,
+    258-281) on the GPU (fac_video_score: per-logit sigmoid, fp32 column sums
+    in crop order, the f > r rule), then the one device->host read the
+    reference makes (.item(), :242)."""
+    logits = logits.float().contiguous()
+    out = torch.empty((), dtype=torch.float32, device=logits.device)
+    _lib.check(_lib.load().fac_video_score(logits.data_ptr(), int(logits.shape[0]), out.data_ptr(),
+                                           torch.cuda.current_stream(logits.device).cuda_stream),
+               None, "fac_video_score")
+    return float(out.item())

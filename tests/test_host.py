@@ -87,7 +87,7 @@ def test_forward_fails_loudly_without_gpu():
     m = CViT()
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 3, 224, 224))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError):   # a mask does not change that (no CPU fallback)
         m(torch.zeros(1, 3, 224, 224), mask=torch.ones(1, 1, dtype=torch.bool))
     with pytest.raises(ValueError):
         m(torch.zeros(1, 3, 112, 112))
@@ -148,3 +148,22 @@ def test_conv3x3_weight_packing_layout(built_lib, H, ci, co):
                     qs = q ^ 2 if (H != 224 and (t // 3) % 2 == 1) else q
                     want = w[nb * bn:(nb + 1) * bn, ch * 32 + qs * 8:ch * 32 + qs * 8 + 8].reshape(bn, 8, 9)[:, :, t]
                     assert torch.equal(got[nb, ch, t, q], want), (nb, ch, t, q)
+
+
+def test_reference_mask_semantics(golden):
+    """cvit.py:50-55's mask=: the host check reproduces the reference's
+    errors (AssertionError for a wrong width, the broadcast RuntimeError for
+    B not in {1, heads}) and which masks poison the logits with NaN
+    (tests/golden/mask_semantics.json, tools/make_golden_mask.py)."""
+    import torch
+    from fac_fake_amd.cvit import reference_mask_poisons
+    for c in golden("mask_semantics.json"):
+        mask = torch.tensor(c["mask"], dtype=torch.bool)
+        if c["outcome"] == "error":
+            exc = {"AssertionError": AssertionError, "RuntimeError": RuntimeError}[c["error"]]
+            with pytest.raises(exc):
+                reference_mask_poisons(mask, c["B"])
+        else:
+            assert reference_mask_poisons(mask, c["B"]) == (c["outcome"] == "nan"), c
+            if c["outcome"] == "nan":
+                assert all(c["nan_rows"])

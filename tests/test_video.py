@@ -167,6 +167,8 @@ def _dense_worker(rank, world, port, frames, boxes, q):
     try:
         import fac_fake_amd.video as v
         v.crop_faces = lambda fr, bx: torch.from_numpy(ov.crop_batch(fr.numpy(), bx))  # CPU stand-in
+        from fac_fake_amd.prediction import pre_process_prediction, pred_sig
+        v.device_video_score = lambda lg: float(pre_process_prediction(pred_sig(lg)))  # CPU stand-in
         score, logits = v.predict_video(_StandInModel(), frames, boxes, mode="dense", return_logits=True)
         q.put((rank, score, logits.numpy()))
     finally:
