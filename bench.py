@@ -398,6 +398,8 @@ def main():
     ap.add_argument("--no-s3d", action="store_true", help="skip the config-4 S3D sub-measurement")
     ap.add_argument("--no-repbn8", action="store_true", help="skip the RepBn8-variant sub-measurement")
     ap.add_argument("--only", choices=["resvitkan", "s3d", "repbn8"], help="run only one sub-measurement (profiling)")
+    ap.add_argument("--s3d-batch", type=int, default=64, help="clips per step of the config-4 S3D measurement")
+    ap.add_argument("--rvk-batch", type=int, default=256, help="crops per step of the config-5 ResVitKan measurement")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="fac_set_option knob (include/fac_cvit.h), repeatable")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
@@ -412,7 +414,7 @@ def main():
     dev = torch.device("cuda", local)
     B = args.batch
     if args.only == "resvitkan":
-        r = resvitkan_measurement(dev, args.dtype, world, B, steps=args.steps, warmup=args.warmup,
+        r = resvitkan_measurement(dev, args.dtype, world, args.rvk_batch, steps=args.steps, warmup=args.warmup,
                                   chunk=args.stem_chunk if args.stem_chunk else None)
         if rank == 0:
             print(json.dumps(r), flush=True)
@@ -423,7 +425,7 @@ def main():
             print(json.dumps(r), flush=True)
         return
     if args.only == "s3d":
-        r = s3d_measurement(dev, args.dtype, world, steps=args.steps, warmup=args.warmup)
+        r = s3d_measurement(dev, args.dtype, world, B=args.s3d_batch, steps=args.steps, warmup=args.warmup)
         if rank == 0:
             print(json.dumps(r), flush=True)
         return
@@ -480,9 +482,9 @@ def main():
         model._release()
         del model
     if not args.no_s3d:
-        line["config4"] = s3d_measurement(dev, args.dtype, world)
+        line["config4"] = s3d_measurement(dev, args.dtype, world, B=args.s3d_batch)
     if not args.no_resvitkan:
-        line["config5"] = resvitkan_measurement(dev, args.dtype, world)
+        line["config5"] = resvitkan_measurement(dev, args.dtype, world, args.rvk_batch)
     if not args.no_repbn8:
         line["variant_repbn8"] = repbn8_measurement(dev, args.dtype, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
