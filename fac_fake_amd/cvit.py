@@ -240,6 +240,35 @@ class CViT(nn.Module):
         logits, _ = self._run(x, x.shape[0], pos_index, u8=False, want_probs=False)
         return logits.fill_(float("nan")) if poison else logits
 
+    def forward_u8_pipelined(self, crops: torch.Tensor, pos_index, chunk: int = 256) -> torch.Tensor:
+        """forward_u8 over more crops than one batch: the crops go in
+        ceil(n/chunk) equal chunks through fac_forward_nhwc_u8_pipelined, so
+        chunk k's encoder + head (on the context's tail stream) overlaps
+        chunk k+1's conv stack; then the current stream waits for every chunk.
+        Logits are bit-identical to one forward_u8 call (a crop's logits do
+        not depend on its batch)."""
+        if crops.dtype != torch.uint8 or crops.dim() != 4 or tuple(crops.shape[1:]) != (224, 224, 3):
+            raise ValueError(f"expected uint8 crops [B,224,224,3], got {crops.dtype} {tuple(crops.shape)}")
+        if not crops.is_cuda:
+            raise RuntimeError("CViT (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
+        x = crops.contiguous()
+        n = int(x.shape[0])
+        lib = self._ensure_ctx(x.device)
+        pidx = self._pos_index(n, pos_index, x.device)
+        logits = torch.empty(n, 2, dtype=torch.float32, device=x.device)
+        if n == 0:
+            return logits
+        k = -(-n // max(1, int(chunk)))
+        step = -(-n // k)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        for lo in range(0, n, step):
+            hi = min(n, lo + step)
+            _lib.check(lib.fac_forward_nhwc_u8_pipelined(self._ctx, x[lo:hi].data_ptr(), hi - lo,
+                                                         pidx[lo:hi].data_ptr(), logits[lo:hi].data_ptr(), None,
+                                                         None, stream), self._ctx, "fac_forward_nhwc_u8_pipelined")
+        _lib.check(lib.fac_pipeline_join(self._ctx, 0, stream), self._ctx, "fac_pipeline_join")
+        return logits
+
     def forward_u8(self, crops: torch.Tensor, pos_index=None, return_probs: bool = False):
         """uint8 NHWC RGB face crops [B,224,224,3] -> logits (and per-logit sigmoids)."""
         if crops.dtype != torch.uint8 or crops.dim() != 4 or tuple(crops.shape[1:]) != (224, 224, 3):

@@ -135,6 +135,10 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         lo, hi = shard_bounds(n, world, rank)
         if hi > lo:
             crops = crop_faces(frames, boxes[lo:hi])
+            # one forward over the rank's crops: splitting them into pipelined
+            # chunks (CViT.forward_u8_pipelined) measured slower for a 300-crop
+            # video (4.73-5.13 vs 4.55 ms: two half batches fill the GPU worse
+            # than their overlap saves; tools/video_breakdown.py)
             with torch.no_grad():
                 local = model.forward_u8(crops, pos_index=torch.from_numpy(dense_slots(hi - lo, offset=lo)))
         else:

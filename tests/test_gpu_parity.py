@@ -471,6 +471,20 @@ def test_pipelined_forward_matches_synchronous(models):
         assert torch.equal(scores[i].cpu(), sc.cpu()), i
 
 
+def test_forward_u8_pipelined_chunks_match(models):
+    """CViT.forward_u8_pipelined (equal chunks through the pipelined C ABI,
+    chunk k's encoder beside chunk k+1's conv stack) == one forward_u8 call,
+    bit for bit, for 2, 5 and 1 chunk(s) and both dtypes."""
+    crops = torch.from_numpy(make_crops(300, seed=31)).to(DEV)
+    slots = torch.from_numpy((np.arange(300) % 32).astype(np.int32))
+    for dt in ("bf16", "fp16"):
+        m = models[dt]
+        ref = m.forward_u8(crops, pos_index=slots).cpu()
+        for chunk in (160, 64, 300):
+            got = m.forward_u8_pipelined(crops, slots, chunk=chunk).cpu()
+            assert torch.equal(got, ref), (dt, chunk)
+
+
 def test_crop_resize_kernel_matches_oracle():
     """fac_crop_resize_u8 (crop + INTER_AREA + BGR->RGB) is bit-identical to
     oracle/video.py on downscales (odd and even sizes; exact-integer area
