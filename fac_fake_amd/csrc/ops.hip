@@ -80,7 +80,13 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                    (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
-template <class T, int BM, int BN, int WM, int WN, int OCC, int NS>
+// UT (uniform tap): cin % 64 == 0, so every K step (64 channels) lies in one
+// tap and the tap / channel offset of a step is the same for every lane: the
+// gather is one precomputed row offset + a wave-uniform step offset per A
+// piece, validity by three unsigned compares, and no per-lane (channel piece,
+// tap) tracking or per-piece branches (the generic path's VALU work was ~8.5
+// instructions per MFMA on the ResNet-50 layers: profiles/r03_resvitkan_pmc.json).
+template <class T, int BM, int BN, int WM, int WN, int OCC, int NS, bool UT = false>
 __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
   constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
   constexpr int BK = 64;
@@ -134,14 +140,50 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
   }
   // this lane's K piece (channel piece, tap), advanced 8 pieces per stage
   Trk t{j, 0, 0, 0, j};
-  trk_norm(t, p.C8, p.KH, p.KW);
+  if constexpr (!UT) trk_norm(t, p.C8, p.KH, p.KW);
   const uint16_t* wsrc[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) wsrc[i] = p.w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * p.Kp + j * 8;
+  // UT: element offset of each A row's tap-(0,0,0) input pixel (+ this lane's
+  // piece), and the wave-uniform step state: channel offset c0, tap (uz,uy,ux)
+  long long roff[UT ? NA : 1];
+  if constexpr (UT) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      roff[i] = (rbase[i] - p.in) + (((long long)riz[i] * p.H + riy[i]) * p.W + rix[i]) * (p.C8 * 8) + j * 8;
+  }
+  int uc = 0, uz = 0, uy = 0, ux = 0;
+  const long long rowstride = (long long)p.W * p.C8 * 8, planestride = rowstride * p.H;
 
   // stage st -> ring slot st % NS; stages past the end copy zeros into slots never read
   auto issue = [&](int st) {
     uint16_t* slot = smem + (st % NS) * SLOT;
+    if constexpr (UT) {
+      const bool real = st < p.ksteps;
+      const long long toff = uz * planestride + uy * rowstride + (long long)ux * p.C8 * 8 + uc;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const bool ok = real & ((unsigned)(riz[i] + uz) < (unsigned)p.D) & ((unsigned)(riy[i] + uy) < (unsigned)p.H) &
+                        ((unsigned)(rix[i] + ux) < (unsigned)p.W);
+        const uint16_t* src = ok ? p.in + (roff[i] + toff) : g_zero16;
+        glds16(src, slot + (NW * i + wave) * 64 * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        glds16(real ? wsrc[i] + (size_t)st * BK : g_zero16, slot + SLOT_A + (NW * i + wave) * 64 * 8);
+      uc += 64;
+      if (uc == p.C8 * 8) {
+        uc = 0;
+        if (++ux == p.KW) {
+          ux = 0;
+          if (++uy == p.KH) {
+            uy = 0;
+            ++uz;
+          }
+        }
+      }
+      return;
+    }
     const bool real = st < p.ksteps && t.kp < p.ktot8;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
@@ -952,30 +994,40 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
   return dim3(gx, ny);
 }
 
-template <class T>
-static hipError_t launch_convnd(ConvP p, int cout_pad, hipStream_t st) {
-  (void)cout_pad;
+template <class T, bool UT>
+static void launch_convnd_t(ConvP p, hipStream_t st) {
   const int gx64 = (p.M + 63) / 64, gx128 = (p.M + 127) / 128, gx256 = (p.M + 255) / 256;
   const int ny64 = (p.Cout + 63) / 64, ny128 = (p.Cout + 127) / 128;
   if (p.ksteps <= 2) {
     // K <= 128 (1x1 expansions): memory-bound, so occupancy first — a 2-slot
     // ring (48 KB) lets three 128 x 64 workgroups share a CU
     const dim3 g = conv_grid(p, gx128, ny64);
-    convnd_igemm<T, 128, 64, 2, 2, 3, 2><<<g, 256, 0, st>>>(p);
+    convnd_igemm<T, 128, 64, 2, 2, 3, 2, UT><<<g, 256, 0, st>>>(p);
   } else if ((long long)gx128 * ny64 < 512) {
     // small grids (S3D's late 4x7x7 / 2x3x3 stages): 64 x 64 tiles, three per CU
     const dim3 g = conv_grid(p, gx64, ny64);
-    convnd_igemm<T, 64, 64, 2, 2, 3, 3><<<g, 256, 0, st>>>(p);
+    convnd_igemm<T, 64, 64, 2, 2, 3, 3, UT><<<g, 256, 0, st>>>(p);
   } else if (p.Cout % 128 == 0 && (long long)gx256 * ny128 >= 448) {
     // 256 x 128 tiles (8 waves, 144 KB ring, one per CU: 48 KB global -> LDS per
     // 4.2 MFLOP, twice the 128 x 64 tile's intensity) when the grid still fills
     // the chip about twice over and no column tile is half empty
     const dim3 g = conv_grid(p, gx256, ny128);
-    convnd_igemm<T, 256, 128, 4, 2, 1, 3><<<g, 512, 0, st>>>(p);
+    convnd_igemm<T, 256, 128, 4, 2, 1, 3, UT><<<g, 512, 0, st>>>(p);
   } else {
     const dim3 g = conv_grid(p, gx128, ny64);
-    convnd_igemm<T, 128, 64, 2, 2, 2, 3><<<g, 256, 0, st>>>(p);
+    convnd_igemm<T, 128, 64, 2, 2, 2, 3, UT><<<g, 256, 0, st>>>(p);
   }
+}
+
+template <class T>
+static hipError_t launch_convnd(ConvP p, int cout_pad, hipStream_t st) {
+  (void)cout_pad;
+  static const bool ut_on = [] {
+    const char* e = std::getenv("FAC_CONV_UT");
+    return !(e && e[0] == '0');
+  }();
+  if (ut_on && p.C8 % 8 == 0) launch_convnd_t<T, true>(p, st);
+  else launch_convnd_t<T, false>(p, st);
   return hipGetLastError();
 }
 

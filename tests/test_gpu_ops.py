@@ -66,6 +66,10 @@ CONV_CASES = [
     (3, 1, 23, 29, 128, 192, (1, 1, 1), 1, 0),
     (1, 1, 56, 56, 64, 256, (1, 1, 1), 1, 0),
     (2, 1, 14, 15, 256, 128, (1, 1, 1), 1, 0),
+    # cin % 64 == 0 on convnd_igemm: the uniform-tap gather (one tap per K step)
+    (2, 4, 9, 11, 64, 128, (3, 3, 3), 1, 1),                 # 3-D taps, padding on every axis
+    (2, 3, 7, 7, 192, 130, (3, 3, 3), (1, 2, 2), (1, 1, 1)),  # ragged cout, strided
+    (4, 1, 112, 256, 320, 128, (1, 1, 1), 1, 0),            # M = 114688: the 256 x 128 tile
 ]
 
 
