@@ -49,7 +49,6 @@ hipError_t launch_crop_resize(const uint8_t* frames, int n_frames, int H, int W,
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
                           hipStream_t s, int* sched = nullptr);
-void set_stem_version(int v);
 enum { EPI_F32 = 0, EPI_F32_RELU = 1, EPI_T_GELU = 2, EPI_RESID = 3, EPI_PARTIAL = 4, EPI_T = 5 };
 }  // namespace fac
 
@@ -723,11 +722,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   }
   if (k == "stem_dynamic") {
     c->stem_dynamic = value != 0;
-    return FAC_OK;
-  }
-  if (k == "stem_version") {  // process-wide: 0 = stem224_fused, 1 = stem224_strip
-    if (value < 0 || value > 1) return set_err(c, FAC_ERR_ARG, "stem_version must be 0 or 1");
-    fac::set_stem_version(value);
     return FAC_OK;
   }
   if (k == "stem_nwg") {

@@ -217,8 +217,10 @@ class S3D(nn.Module):
             main.wait_stream(s)
         return out
 
-    def features16(self, x16: torch.Tensor) -> torch.Tensor:
-        """`base` (model.py:17-33) on the packed clip -> [B, T', H', W', 1024] 16-bit."""
+    def features16(self, x16: torch.Tensor, taps: list | None = None) -> torch.Tensor:
+        """`base` (model.py:17-33) on the packed clip -> [B, T', H', W', 1024] 16-bit.
+        With `taps`, the output of every base[i] ([B, T, H, W, C] channels-last,
+        16-bit) is appended to it, in order."""
         y = x16
         if self._srm_conv is not None:
             n, d, h, w, _ = y.shape
@@ -233,19 +235,32 @@ class S3D(nn.Module):
                 y = max_pool_sep(y, *L)
             else:
                 y = self._mixed(y, L)
+            if taps is not None:
+                taps.append(y)
         return y
 
-    def forward(self, x: torch.Tensor, return_probs: bool = False):
+    def _pack(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
             raise RuntimeError("S3D (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
         if x.dim() != 5 or x.shape[1] != 3:
             raise ValueError(f"expected a clip [B,3,T,H,W], got {tuple(x.shape)}")
         self._prepare(x.device)
-        B, _, T, H, W = x.shape
+        _, _, T, H, W = x.shape
         if self._srm:
-            x16 = pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
-        else:
-            x16 = pack_input_s2d(x.float(), dtype=self.dtype_name, u8=False, pad_before=2, pad_after=1)
+            return pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
+        return pack_input_s2d(x.float(), dtype=self.dtype_name, u8=False, pad_before=2, pad_after=1)
+
+    def base_outputs(self, x: torch.Tensor) -> list:
+        """The output of every base[i] (model.py:17-33) for the raw clip `x`,
+        channels-last 16-bit: what a forward hook on the reference's
+        ``base[i]`` sees, for per-block parity checks."""
+        taps = []
+        self.features16(self._pack(x), taps)
+        return taps
+
+    def forward(self, x: torch.Tensor, return_probs: bool = False):
+        x16 = self._pack(x)
+        B = x.shape[0]
         y = self.features16(x16)
         _, t, h, w, _ = y.shape
         y = pool(y, (2, h, w), 1, 0, "avg")                           # F.avg_pool3d(y, (2, H, W), stride=1)
@@ -254,4 +269,41 @@ class S3D(nn.Module):
         return (logits, sigmoid(logits)) if return_probs else logits
 
 
-__all__ = ["S3D", "TORCH16"]
+def custom_round(values):
+    """utils.py:25-32: 1 where a value is > 0.5, else 0."""
+    return (torch.as_tensor(values, dtype=torch.float64) > 0.5).to(torch.int64).numpy()
+
+
+def custom_video_round(preds):
+    """utils.py:34-38: the first value > 0.5, else the mean."""
+    for p in preds:
+        if p > 0.5:
+            return p
+    return sum(preds) / len(preds)
+
+
+def video_predictions(model: S3D, snippets: torch.Tensor, batch: int = 64) -> list:
+    """The per-video score of S3D-test.py's modeleval (:259-283) for a batch of
+    videos, one snippet each (read_frames keeps every 10th of the first 200
+    frames: one [3, 20, H, W] snippet per video, :185-195), as a list of
+    floats.  Per video the reference takes ``sigmoid`` of each row of the
+    model's output, their mean, element [0] (:269-276), and
+    ``custom_video_round`` only when a video has more than one face
+    prediction, which one snippet never has (:280-283).  Snippets run through
+    the drop-in in batches of `batch` clips; each video's logits are
+    independent of its batch neighbours."""
+    if snippets.dim() != 5:
+        raise ValueError(f"expected snippets [V,3,T,H,W], got {tuple(snippets.shape)}")
+    out = []
+    for v0 in range(0, snippets.shape[0], batch):
+        _, probs = model(snippets[v0:v0 + batch], return_probs=True)
+        for p in probs.double().cpu():
+            faces_preds = [p]                                   # one snippet = one prediction row
+            cur = sum(faces_preds) / len(faces_preds)
+            video_faces_preds = [float(cur[0])]
+            out.append(custom_video_round(video_faces_preds) if len(video_faces_preds) > 1
+                       else video_faces_preds[0])
+    return out
+
+
+__all__ = ["S3D", "TORCH16", "custom_round", "custom_video_round", "video_predictions"]

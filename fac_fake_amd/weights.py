@@ -378,6 +378,29 @@ def s3d_clips(n: int, frames: int, size: int, seed: int) -> np.ndarray:
     return (z >> np.uint64(56)).astype(np.float32).reshape(n, 3, frames, size, size)
 
 
+def s3d_clips_varied(n: int, frames: int, size: int, seed: int) -> np.ndarray:
+    """n raw clips [n, 3, frames, size, size] (float32 integers 0..255) that
+    differ in content, not only in noise: clip k blends a moving colour
+    wave (per-clip direction, speed, phase and brightness; all on a 2^-24
+    grid from ``uniform``, so every platform computes the same pixels) with
+    uniform noise at weight k/(n-1).  Uniform-noise clips drive every clip to
+    almost the same logit; these spread them."""
+    p = uniform("clip_params", n * 8, seed).astype(np.float64).reshape(n, 8)
+    noise = s3d_clips(n, frames, size, seed).astype(np.float64)
+    t = np.arange(frames, dtype=np.float64)[:, None, None] / frames
+    yy = np.arange(size, dtype=np.float64)[None, :, None] / size
+    xx = np.arange(size, dtype=np.float64)[None, None, :] / size
+    out = np.empty((n, 3, frames, size, size), np.float32)
+    for k in range(n):
+        a, b, c, ph, br, amp = 3 * p[k, 0], 3 * p[k, 1], 2 * p[k, 2], np.pi * p[k, 3], 40 * p[k, 4], 60 + 30 * p[k, 5]
+        alpha = k / max(n - 1, 1)
+        for ch in range(3):
+            wave = 128 + br + amp * np.sin(2 * np.pi * (a * xx + b * yy + c * t) + ph + 2.1 * ch)
+            v = (1 - alpha) * wave + alpha * noise[k, ch]
+            out[k, ch] = np.clip(np.rint(v), 0, 255)
+    return out
+
+
 # ---------------------------------------------------------------- CViT RepBn8
 # CViT-main/model/cvit_GGCA_ADD_DEConv_RepBn8.py::CViT (:343-455): the CViT
 # stem with DEConv blocks (:320-340, five parallel 3x3 / 1-D kernels summed

@@ -45,7 +45,9 @@ def _sep(sd, p, x, k, s, pd):
 
 
 @torch.no_grad()
-def features_fp32(sd, x: torch.Tensor, srm: bool) -> torch.Tensor:
+def features_fp32(sd, x: torch.Tensor, srm: bool, taps: list | None = None) -> torch.Tensor:
+    """`base` (model.py:17-33); with `taps`, every base layer's output
+    [B, C, T, H, W] is appended to it (the reference module's base[i] outputs)."""
     sd = to_torch_sd(sd)
     y = F.conv3d(x.float(), sd["SRM.hpf.weight"], padding=(0, 2, 2)) if srm else x.float()
     for i, L in enumerate(s3d_base(srm)):
@@ -62,6 +64,8 @@ def features_fp32(sd, x: torch.Tensor, srm: bool) -> torch.Tensor:
             y2 = _sep(sd, f"{p}.branch2.1", _basic(sd, f"{p}.branch2.0", y), 3, 1, 1)
             y3 = _basic(sd, f"{p}.branch3.1", F.max_pool3d(y, 3, 1, 1))
             y = torch.cat((y0, y1, y2, y3), 1)
+        if taps is not None:
+            taps.append(y)
     return y
 
 
@@ -84,7 +88,8 @@ def _fold(sd, ck, bn):
 
 
 @torch.no_grad()
-def forward_emulated(sd, x: torch.Tensor, srm: bool, dtype: str = "bf16") -> torch.Tensor:
+def features_emulated(sd, x: torch.Tensor, srm: bool, dtype: str = "bf16", taps: list | None = None) -> torch.Tensor:
+    """`base` at the gfx950 path's rounding points; `taps` as in features_fp32."""
     sd = to_torch_sd(sd)
     r = lambda t: round_to(t, dtype)  # noqa: E731
 
@@ -116,6 +121,16 @@ def forward_emulated(sd, x: torch.Tensor, srm: bool, dtype: str = "bf16") -> tor
             y2 = sep(f"{p}.branch2.1", basic(f"{p}.branch2.0", y), 3, 1, 1)
             y3 = basic(f"{p}.branch3.1", F.max_pool3d(y, 3, 1, 1))
             y = torch.cat((y0, y1, y2, y3), 1)
+        if taps is not None:
+            taps.append(y)
+    return y
+
+
+@torch.no_grad()
+def forward_emulated(sd, x: torch.Tensor, srm: bool, dtype: str = "bf16") -> torch.Tensor:
+    sd = to_torch_sd(sd)
+    r = lambda t: round_to(t, dtype)  # noqa: E731
+    y = features_emulated(sd, x, srm, dtype)
     y = r(F.avg_pool3d(y, (2, y.size(3), y.size(4)), stride=1))
     y = r(y.mean(2, keepdim=True))
     y = F.conv3d(y, r(sd["fc.0.weight"]), sd["fc.0.bias"])

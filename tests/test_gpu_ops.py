@@ -288,6 +288,55 @@ def test_s3d_matches_reference(s3d_models, golden, srm, dt, tol):
     assert np.abs(pr.cpu().numpy() - p_ref).max() <= tol
 
 
+def _rel_to_rms(got, ref):
+    return float(np.abs(got - ref).max() / (np.sqrt((ref.astype(np.float64) ** 2).mean()) + 1e-30))
+
+
+@pytest.mark.parametrize("srm", ["no", "yes"])
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_s3d_every_block_matches_reference(s3d_models, golden, srm, dt):
+    """8 content-varied clips: the per-channel means of EVERY base[i] output
+    (stem convs, pools, each Mixed_* block's four concatenated branches) against
+    the reference module's (tests/golden/s3d_golden_blocks.npz), within 2x the
+    16-bit rounding envelope of that layer (the oracle's emulation of the HIP
+    path's rounding points vs fp32, stored with the fixture).  A wrong branch,
+    channel slot or stride moves a layer's channel means by O(rms), far past
+    the 0.1-6 % envelopes.  Probabilities: fp16 within 1e-3 (the north-star
+    bar), bf16 within 2x its emulated envelope."""
+    from fac_fake_amd.weights import s3d_clips_varied
+    g = golden("s3d_golden_blocks.npz")
+    x = torch.from_numpy(s3d_clips_varied(int(g["n_clips"]), 16, 112, int(g["clip_seed"]))).to(DEV)
+    m = s3d_models[(srm, dt)]
+    taps = m.base_outputs(x)
+    torch.cuda.synchronize()
+    assert len(taps) == 16
+    env = g[f"env_{srm}_{dt}"]
+    for i, t in enumerate(taps):
+        got = t.float().mean(dim=(1, 2, 3)).double().cpu().numpy()
+        ref = g[f"mean_{srm}_{i}"].astype(np.float64)
+        assert got.shape == ref.shape, (i, got.shape, ref.shape)
+        err = _rel_to_rms(got, ref)
+        assert err <= 2 * env[i] + 1e-4, (i, err, env[i])
+    lg, pr = m(x, return_probs=True)
+    p_ref = 1 / (1 + np.exp(-g[f"logits_{srm}"].astype(np.float64)))
+    bar = 1e-3 if dt == "fp16" else 2 * float(g[f"env_prob_{srm}_{dt}"])
+    assert np.abs(pr.double().cpu().numpy() - p_ref).max() <= bar
+
+
+def test_s3d_video_predictions(s3d_models, golden):
+    """S3D-test.py's per-video score (sigmoid per row, mean, [0]) for 8 videos of
+    one snippet each, in batches of 3 (ragged last batch): the reference's
+    probabilities within 1e-3 (fp16) and custom_round's labels."""
+    from fac_fake_amd.s3d import custom_round, video_predictions
+    from fac_fake_amd.weights import s3d_clips_varied
+    g = golden("s3d_golden_blocks.npz")
+    x = torch.from_numpy(s3d_clips_varied(int(g["n_clips"]), 16, 112, int(g["clip_seed"]))).to(DEV)
+    preds = video_predictions(s3d_models[("no", "fp16")], x, batch=3)
+    p_ref = 1 / (1 + np.exp(-g["logits_no"].astype(np.float64)))[:, 0]
+    assert len(preds) == 8 and np.abs(np.array(preds) - p_ref).max() <= 1e-3
+    assert np.array_equal(custom_round(preds), custom_round(p_ref))
+
+
 def test_s3d_matches_emulation_tightly(s3d_models, golden):
     """fp16 path vs the oracle's emulation of its rounding points: logits within 2e-3."""
     from oracle import s3d_torch as O

@@ -44,3 +44,33 @@ def test_emulation_within_16bit_envelope(golden, torch_threads, srm):
     for dt, tol in (("fp16", 1e-3), ("bf16", 1e-2)):
         p = torch.sigmoid(O.forward_emulated(sd, x, srm == "yes", dt))
         assert (p - p_ref).abs().max() <= tol, dt
+
+
+@pytest.mark.parametrize("srm", ["no", "yes"])
+def test_oracle_every_block_matches_reference(golden, torch_threads, srm):
+    """The oracle's base[i] outputs on the 8 content-varied clips: per-channel
+    means equal to the reference module's (s3d_golden_blocks.npz) to fp32
+    summation-order noise, and the fixture's logits spread (a fixture whose
+    clips all score alike pins little)."""
+    from oracle import s3d_torch as O
+    from fac_fake_amd.weights import s3d_clips_varied
+    g = golden("s3d_golden_blocks.npz")
+    x = torch.from_numpy(s3d_clips_varied(int(g["n_clips"]), 16, 112, int(g["clip_seed"])))
+    taps = []
+    O.features_fp32(make_s3d_state_dict(0, 1, srm == "yes"), x, srm == "yes", taps)
+    assert len(taps) == 16
+    for i, t in enumerate(taps):
+        got = t.double().mean(dim=(2, 3, 4)).numpy()
+        ref = g[f"mean_{srm}_{i}"].astype(np.float64)
+        assert np.abs(got - ref).max() <= 1e-5 * np.sqrt((ref ** 2).mean()) + 1e-7, i
+    p = 1 / (1 + np.exp(-g[f"logits_{srm}"].astype(np.float64)))
+    assert p.max() - p.min() > 0.03
+
+
+def test_custom_round_semantics():
+    """utils.py:25-38 (S3D harness): strict > 0.5 threshold; the first
+    prediction above 0.5 wins, else the mean."""
+    from fac_fake_amd.s3d import custom_round, custom_video_round
+    assert list(custom_round([0.2, 0.5, 0.50001, 0.9])) == [0, 0, 1, 1]
+    assert custom_video_round([0.1, 0.7, 0.9]) == 0.7
+    assert abs(custom_video_round([0.1, 0.3]) - 0.2) < 1e-12
