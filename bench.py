@@ -408,9 +408,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("FAC_DIST_BACKEND", "nccl") != "nccl":
+        local %= max(torch.cuda.device_count(), 1)   # rehearsal: several ranks may share a GPU
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL over xGMI; FAC_DIST_BACKEND=gloo only to rehearse the multi-rank
+        # control flow with several ranks on one GPU (RCCL refuses that)
+        backend = os.environ.get("FAC_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     B = args.batch
     if args.only == "resvitkan":
