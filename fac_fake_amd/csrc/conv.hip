@@ -489,7 +489,8 @@ namespace fac {
 //        4 workgroups per CU
 //    56:  8x28 box, BN 128, 2x2 waves (224 rows, no padding)
 //    28:  4x28 box, BN 256, 1x4 waves (112 rows, no padding)
-//    14: 14x14 box, BN 128, 1x4 waves (208 rows for 196 pixels)
+//    14: 14x14 box, BN 128, 1x4 waves (208 rows for 196 pixels); BN 192 / 64
+//        for S3D's 14^2 (1,3,3) convs with cout 192 / 320 (round 3)
 // (the 224 layers normally run inside stem224.hip; the 16x16/BN 32 kernel
 // serves the unfused debug path)
 //
@@ -502,21 +503,29 @@ int conv_block_n(int H, int cout) {
     case 112: return cout % 64 == 0 ? 64 : 0;
     case 56: return cout % 128 == 0 ? 128 : (cout % 64 == 0 ? 64 : 0);
     case 28: return cout % 256 == 0 ? 256 : (cout % 192 == 0 ? 192 : (cout % 128 == 0 ? 128 : 0));
-    case 14: return cout % 128 == 0 ? 128 : 0;
+    case 14: return cout % 128 == 0 ? 128 : (cout % 192 == 0 ? 192 : (cout % 64 == 0 ? 64 : 0));
     default: return 0;
   }
 }
 
-template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true>
-static void launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
-                       int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
+// POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
+// spill with it; no model pools after such a layer)
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true>
+static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
+                             int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
-  if (pool)
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
-        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
-  else
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
-        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  if constexpr (POOLED) {
+    if (pool) {
+      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
+          <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+      return hipSuccess;
+    }
+  } else if (pool) {
+    return hipErrorInvalidValue;
+  }
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
+      <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  return hipSuccess;
 }
 
 template <class T>
@@ -535,6 +544,11 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
     case 28192: launch_box<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28128: launch_box<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 14128: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 14192:
+      if (launch_box<T, 14, 14, 192, 1, 4, 2, 2, false, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
+        return hipErrorInvalidValue;
+      break;
+    case 14064: launch_box<T, 14, 14, 64, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

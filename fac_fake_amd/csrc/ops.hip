@@ -897,12 +897,17 @@ template <class T>
 __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
                                                   const float* __restrict__ bias, uint16_t* __restrict__ out,
                                                   int nunits, int S, int D, int Cin, int kd, int sd, int pd, int kp,
-                                                  int ldo, int c_off, int relu_on, int db) {
+                                                  int ldo, int c_off, int relu_on, int db, int nbk, int nslot) {
   constexpr int LDS_EL = 81920;  // 160 KiB
   __shared__ __attribute__((aligned(16))) uint16_t smem[LDS_EL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int nb = blockIdx.y;
+  // workgroup -> (unit slot, 64-channel block): the nbk blocks of one slot
+  // have ids 8 apart (same XCD under round-robin placement, dispatched
+  // together), so they read each unit's input slab from HBM once and share
+  // it through that XCD's L2 instead of streaming the whole input nbk times
+  const int b_lo = blockIdx.x & 7, b_hi = blockIdx.x >> 3;
+  const int nb = b_hi % nbk, slot = (b_hi / nbk) * 8 + b_lo;
   const int NP = Cin >> 3, CH = Cin >> 5, KS = kd * CH;  // pieces / 32-channel chunks per position, k-steps
   const int SLAB = D * 16 * Cin;                          // elements per slab buffer
   uint16_t* const wts = smem;
@@ -922,7 +927,7 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
     }
   };
 
-  int u = blockIdx.x;
+  int u = slot;
   if (u < nunits) issue_slab(slab0, u);
   // this workgroup's 64 output channels, all k-steps
   for (int c = tid; c < 64 * KS * 4; c += 512) {
@@ -937,7 +942,7 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
     for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[nb * 64 + ct * 16 + 4 * g + j] : 0.f;
   const int z = wave;  // output frame of this wave (Do == 8)
   for (int it = 0; u < nunits; ++it) {
-    const int next = u + gridDim.x;
+    const int next = u + nslot;
     uint16_t* const cur = slab0 + (db == 2 ? (it & 1) * SLAB : 0);
     // slab u in; the other buffer's readers done.  lgkmcnt(0) too: the weight
     // block above was written with plain ds_writes, which must have landed
@@ -977,6 +982,202 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
     }
     u = next;
   }
+}
+
+// ---- conv_tk2 (round 3): the same temporal convs as conv_tk, with the unit's
+// input streamed as K slices instead of one whole slab.  conv_tk copies a
+// unit's D x 16 x Cin slab and then computes on it; for Cin 192 the slab
+// (48 KB) and the 64-channel weight block (72 KB) leave no room for a second
+// slab, so every unit waited for its slab (base.3's (3,1,1) 192->192 at
+// 8x28^2: 0.73 ms for 0.15 ms of HBM and MFMA work).  Here the K loop runs
+// 32-channel chunk outer, tap inner: slice c of a unit is D frames x 16
+// positions x 32 channels (D KB), all that chunk's taps need, and slices
+// stream continuously across units through a 3-slot ring, two ahead of the
+// MFMAs, with hand-counted vmcnt waits (DP glds pieces per thread per slice,
+// plus the 4 output stores of a unit's last slice).  Positions in a frame
+// row are 64 B; piece j of position p sits at 16-byte slot 4p + (j ^ ((p >> 1)
+// & 2)), which makes every ds_read_b128 lane group of a fragment read (16
+// positions x piece g) hit 16 distinct 4-bank groups.  Wave z computes output
+// frame z (Do == 8) for the unit's 16 positions x the workgroup's 64
+// channels, MFMAs transposed as in conv_tk; the nbk column blocks of a unit
+// slot are 8 workgroup ids apart (see conv_tk).
+// vmcnt(BASE + 4k) for the wave-uniform k in 0..K (s_waitcnt takes an immediate)
+template <int BASE, int K>
+__device__ __forceinline__ void wait_vm_stores(int k) {
+  if constexpr (K > 0) {
+    if (k < K) {
+      wait_vm_stores<BASE, K - 1>(k);
+      return;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(BASE + 4 * K) : "memory");
+}
+
+#ifdef TK2_STAMPS
+__device__ unsigned long long tk2_st[4][64][8][4];
+#define TK2_STAMP(k)                                                                          \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long t_;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (blockIdx.x < 4 && lane == 0 && s < 64) tk2_st[blockIdx.x][s][wave][(k)] = t_;         \
+  } while (0)
+#else
+#define TK2_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
+template <class T, int DP, int KD, int SD, int KC, int R>
+__global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                   const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                   int nunits, int S, int Cin, int kp, int ldo, int c_off, int relu_on,
+                                                   int nbk, int nslot) {
+  constexpr int D = DP * 8;             // input frames: one glds piece per thread per chunk per 8 frames
+  constexpr int PD = KD / 2;            // 'same' temporal padding (model.py:63-82)
+  constexpr int NF = SD + KD;           // input frames two consecutive output frames span
+  constexpr int CE = D * 16 * 32;       // elements of one 32-channel chunk of a unit
+  constexpr int SL = KC * CE;           // slice (one step) elements
+  constexpr int NP = DP * KC;           // glds pieces per thread per slice
+  constexpr int LDS_EL = 81920;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[LDS_EL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int b_lo = blockIdx.x & 7, b_hi = blockIdx.x >> 3;
+  const int nb = b_hi % nbk, slot = (b_hi / nbk) * 8 + b_lo;
+  const int CH = Cin >> 5, KS = KD * CH, SPU = CH / KC;  // chunks, k-steps, steps per unit
+  const int upc = (S + 15) >> 4;  // units per clip (the last one may be partial)
+  uint16_t* const wts = smem;
+  float* const bsm = (float*)(smem + KS * 2048);
+  uint16_t* const ring = smem + KS * 2048 + 128;
+  const int my_units = slot < nunits ? (nunits - slot + nslot - 1) / nslot : 0;
+  const int nsteps = my_units * SPU;
+
+  // This thread's glds pieces: slice slot sl = k*512 + tid -> (chunk kc,
+  // frame d, position p, channel piece j), the same for every slice; per
+  // slice only the unit (clip n, first position p0) and the chunk group
+  // move, tracked by an incremental cursor (no per-step divisions).
+  int toff[NP], tp[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int sl = k * 512 + tid;
+    const int kc = sl / (D * 64), r1 = sl - kc * (D * 64);
+    const int d = r1 >> 6, rem = r1 & 63, p = rem >> 2, j = (rem & 3) ^ ((p >> 1) & 2);
+    toff[k] = (d * S + p) * Cin + kc * 32 + j * 8;
+    tp[k] = p;
+  }
+  int is = 0, ic = 0, iu = slot;
+  int in_ = iu / upc, ip0 = (iu - in_ * upc) << 4;
+  auto issue = [&]() {  // slice `is` (past the last step: zero pieces, so every step issues the same count)
+    uint16_t* dst = ring + (is % R) * SL;
+    const bool live = is < nsteps;
+    const uint16_t* ub = in + ((size_t)in_ * D * S + ip0) * Cin + ic * KC * 32;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const uint16_t* src = live && ip0 + tp[k] < S ? ub + toff[k] : g_zero16;
+      glds16(src, dst + (k * 512 + wave * 64) * 8);
+    }
+    ++is;
+    if (++ic == SPU) {
+      ic = 0;
+      iu += nslot;
+      in_ = iu / upc;
+      ip0 = (iu - in_ * upc) << 4;
+    }
+  };
+
+  // weight block [k-step t*CH + c][ct][g][r16][8] and biases to LDS (global
+  // loads retired here, before the first glds: the loop's counted waits then
+  // see only slice pieces and output stores)
+  for (int c = tid; c < 64 * KS * 4; c += 512) {
+    const int n = c / (KS * 4), k8 = c - n * (KS * 4);
+    *(u16x8*)(wts + ((((k8 >> 2) * 4 + (n >> 4)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+        *(const u16x8*)(w + (size_t)(nb * 64 + n) * kp + k8 * 8);
+  }
+  if (tid < 64) bsm[tid] = bias ? bias[nb * 64 + tid] : 0.f;
+  __syncthreads();
+  // wave (fp, h): output frames 2fp, 2fp+1 x channels 32h .. 32h+31 (tiles 2h, 2h+1)
+  const int fp = wave & 3, h = wave >> 2;
+  f32x4 bv[2];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) bv[cc] = *(const f32x4*)(bsm + h * 32 + cc * 16 + 4 * g);
+#pragma unroll
+  for (int i = 0; i < R - 1; ++i) issue();
+  const int d0 = 2 * fp * SD - PD;  // input frame of frame 2fp's tap 0
+  const int rdoff = r16 * 32 + ((g ^ ((r16 >> 1) & 2)) << 3);  // this lane's piece in a frame row
+  const uint16_t* const wl = wts + (h * 2 * 4 + g) * 128 + r16 * 8;  // + kstep*2048 + cc*512
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = (f32x4)0.f;
+  // hist bit i: step s-1-i ended a unit (issued its 4 output stores, after
+  // that step's slice issue)
+  unsigned hist = 0;
+  int cs = 0, cu = slot;  // compute cursor: step within the unit, unit
+  for (int s = 0; s < nsteps; ++s) {
+    // slice s landed: younger than it are slices s+1 .. s+R-2 and the output
+    // stores of steps s-R+1 .. s-1; every wave is done with slice s-1's slot,
+    // which this step's issue refills
+    TK2_STAMP(0);
+    wait_vm_stores<(R - 2) * NP, R - 1>(__builtin_popcount(hist & ((1u << (R - 1)) - 1)));
+    TK2_STAMP(1);
+    issue();  // slice s + R - 1
+    TK2_STAMP(2);
+    const uint16_t* const sbase = ring + (s % R) * SL + rdoff;
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int c = cs * KC + kc;
+      const uint16_t* cur = sbase + kc * CE;
+      // every input frame the wave's two output frames read, once (sd = 1:
+      // frame 2fp+1's tap t is frame 2fp's tap t+1), then the weights
+      u16x8 px[NF], wf[KD][2];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int d = d0 + f;
+        px[f] = (unsigned)d < (unsigned)D ? *(const u16x8*)(cur + d * 512) : (u16x8)0;
+      }
+#pragma unroll
+      for (int t = 0; t < KD; ++t)
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) wf[t][cc] = *(const u16x8*)(wl + (t * CH + c) * 2048 + cc * 512);
+#pragma unroll
+      for (int t = 0; t < KD; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int f = j * SD + t;
+          if ((unsigned)(d0 + f) < (unsigned)D) {  // zero padding: no MFMA (wave-uniform)
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) acc[j][cc] = T::mfma(wf[t][cc], px[f], acc[j][cc]);
+          }
+        }
+    }
+    TK2_STAMP(3);
+    const bool stored = cs == SPU - 1;
+    hist = (hist << 1) | (stored ? 1u : 0u);
+    if (stored) {
+      const int n = cu / upc, p0 = (cu - n * upc) << 4;
+      if (p0 + r16 < S) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          uint16_t* o = out + (((size_t)n * 8 + 2 * fp + j) * S + p0 + r16) * ldo + c_off + nb * 64 + h * 32 + 4 * g;
+#pragma unroll
+          for (int cc = 0; cc < 2; ++cc) {
+            f32x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = relu_on ? relu(acc[j][cc][q] + bv[cc][q]) : acc[j][cc][q] + bv[cc][q];
+            *(u16x4*)(o + cc * 16) = T::pack4(v);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = (f32x4)0.f;
+      cs = 0;
+      cu += nslot;
+    } else {
+      ++cs;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero slices landed before LDS is released
 }
 
 // grid of gx row tiles x ny column tiles: flat (column tiles of a row tile
@@ -1185,22 +1386,65 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
       (d->flags & ~FAC_CONV_RELU) == 0 && k_pad == d->kd * d->cin) {
     const int ks = d->kd * d->cin / 32, slab = d->d * 16 * d->cin;
     const int db = ks * 2048 + 2 * slab <= 81920 ? 2 : (ks * 2048 + slab <= 81920 ? 1 : 0);
+    static const bool tk2_on = [] {
+      const char* e = std::getenv("FAC_TK2");
+      return !(e && e[0] == '0');
+    }();
+    const bool k3 = d->kd == 3 && d->sd == 1 && d->pd == 1 && d->d == 8;
+    const bool k7 = d->kd == 7 && d->sd == 2 && d->pd == 3 && d->d == 16;
+    // slices of KC 32-channel chunks (every chunk of a unit in one or two
+    // steps: fewer per-step barriers and slice issues per MFMA), 3 ring slots
+    const int tk2_kc = d->cin == 192 ? 3 : (d->cin == 128 ? 4 : 2);
+    if (tk2_on && (k3 || k7) && (d->cin == 64 || d->cin == 128 || d->cin == 192) &&
+        ks * 2048 + 128 + 3 * tk2_kc * d->d * 512 <= 81920 &&
+        d->cin >= 64) {  // >= 2 slices per unit: at most R/2 store batches per wait window
+      int dev = 0, ncu = 256;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        ncu = 256;
+      const int nunits = d->n * ((d->h * d->w + 15) / 16);
+      const int nbk = d->cout / 64;
+      const int nslot = (std::min(nunits, ncu) + 7) / 8 * 8;
+      const dim3 grid(nslot * nbk);
+      const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
+#define FAC_TK2(TT, DP, KD, SD, KC)                                                                          \
+  conv_tk2<TT, DP, KD, SD, KC, 3><<<grid, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,  \
+                                                 (uint16_t*)d->out, nunits, d->h * d->w, d->cin, k_pad, d->ldo, \
+                                                 d->c_off, relu_on, nbk, nslot)
+      if (d->dtype == FAC_DTYPE_BF16) {
+        if (k7) FAC_TK2(BF16, 2, 7, 2, 2);
+        else if (tk2_kc == 3) FAC_TK2(BF16, 1, 3, 1, 3);
+        else if (tk2_kc == 4) FAC_TK2(BF16, 1, 3, 1, 4);
+        else FAC_TK2(BF16, 1, 3, 1, 2);
+      } else {
+        if (k7) FAC_TK2(F16, 2, 7, 2, 2);
+        else if (tk2_kc == 3) FAC_TK2(F16, 1, 3, 1, 3);
+        else if (tk2_kc == 4) FAC_TK2(F16, 1, 3, 1, 4);
+        else FAC_TK2(F16, 1, 3, 1, 2);
+      }
+#undef FAC_TK2
+      return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+    }
     if (db) {
       int dev = 0, ncu = 256;
       if (hipGetDevice(&dev) != hipSuccess ||
           hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
         ncu = 256;
       const int nunits = d->n * ((d->h * d->w + 15) / 16);
-      const dim3 grid(std::min(nunits, ncu), d->cout / 64);
+      const int nbk = d->cout / 64;
+      // unit slots: a multiple of 8 (slot = 8 * hi + lo, see conv_tk), at most
+      // one per CU and per unit
+      const int nslot = (std::min(nunits, ncu) + 7) / 8 * 8;
+      const dim3 grid(nslot * nbk);
       const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
       if (d->dtype == FAC_DTYPE_BF16)
         conv_tk<BF16><<<grid, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
                                             (uint16_t*)d->out, nunits, d->h * d->w, d->d, d->cin, d->kd, d->sd,
-                                            d->pd, k_pad, d->ldo, d->c_off, relu_on, db);
+                                            d->pd, k_pad, d->ldo, d->c_off, relu_on, db, nbk, nslot);
       else
         conv_tk<F16><<<grid, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
                                            (uint16_t*)d->out, nunits, d->h * d->w, d->d, d->cin, d->kd, d->sd,
-                                           d->pd, k_pad, d->ldo, d->c_off, relu_on, db);
+                                           d->pd, k_pad, d->ldo, d->c_off, relu_on, db, nbk, nslot);
       return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
     }
   }
