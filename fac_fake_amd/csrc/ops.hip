@@ -780,17 +780,24 @@ __global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ i
   const int n0 = blockIdx.y * 64;
   const bool relu_on = flags & FAC_CONV_RELU, relu2 = flags & FAC_CONV_RELU2;
 
-  // weights [s][ct][g][r16][8]: one contiguous 1 KB fragment per (k-step, channel tile)
+  // weights [s][ct][g][r16][8]: one contiguous 1 KB fragment per (k-step,
+  // channel tile).  Row i of channel tile ct computes channel pw_ch(ct, i) =
+  // 32 (ct >> 1) + 8 (i >> 2) + 4 (ct & 1) + (i & 3), so lane group g ends
+  // with channels 8g .. 8g+7 (tiles 0, 1) and 32+8g .. 32+8g+7 (tiles 2, 3)
+  // of its position: two 16-byte stores, and each store instruction writes
+  // 64 contiguous bytes per position (4-channel, 8-byte lanes gave 32-byte
+  // segments)
   for (int c = tid; c < 64 * PPR; c += 256) {
     const int n = c / PPR, k8 = c - n * PPR;
-    *(u16x8*)(sw + ((((k8 >> 2) * 4 + (n >> 4)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+    const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
+    *(u16x8*)(sw + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) =
         *(const u16x8*)(w + (size_t)(n0 + n) * kp + k8 * 8);
   }
   float bv[4][4];
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[n0 + ct * 16 + 4 * g + j] : 0.f;
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[n0 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
   // this lane's glds slots: row and (logical) piece, fixed across tiles
   int arow[PER], aoff[PER];
 #pragma unroll
@@ -827,15 +834,15 @@ __global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ i
     } else {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    // residual vectors to registers before the barrier that frees the buffer
-    u16x4 rv[RT][4];
+    // residual vectors to registers before the barrier that frees the buffer:
+    // channels 8g .. 8g+7 (piece g) and 32+8g .. (piece 4+g) of the lane's position
+    u16x8 rv[RT][2];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int hh = 0; hh < 2; ++hh) {
         const int r = (wave * RT + rt) * 16 + r16;
-        rv[rt][ct] = RES ? *(const u16x4*)(sr + buf * REL + r * 64 + (((ct * 2 + (g >> 1)) ^ (r & 7)) << 3) + (g & 1) * 4)
-                         : (u16x4)0;
+        rv[rt][hh] = RES ? *(const u16x8*)(sr + buf * REL + r * 64 + (((hh * 4 + g) ^ (r & 7)) << 3)) : (u16x8)0;
       }
     const uint16_t* a = sa + buf * AEL;
     f32x4 acc[RT][4];
@@ -861,19 +868,25 @@ __global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ i
     for (int rt = 0; rt < RT; ++rt) {
       const int m = mrow + rt * 16;
       if (m >= M) continue;
-      uint16_t* o = out + (size_t)m * ldo + c_off + n0 + 4 * g;
+      uint16_t* o = out + (size_t)m * ldo + c_off + n0 + 8 * g;
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        f32x4 v;
+      for (int hh = 0; hh < 2; ++hh) {
+        u16x4 q[2];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float x = acc[rt][ct][j] + bv[ct][j];
-          if (relu_on) x = relu(x);
-          if constexpr (RES) x += T::to_f32(rv[rt][ct][j]);
-          if (relu2) x = relu(x);
-          v[j] = x;
+        for (int e = 0; e < 2; ++e) {
+          const int ct = 2 * hh + e;
+          f32x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float x = acc[rt][ct][j] + bv[ct][j];
+            if (relu_on) x = relu(x);
+            if constexpr (RES) x += T::to_f32(rv[rt][hh][4 * e + j]);
+            if (relu2) x = relu(x);
+            v[j] = x;
+          }
+          q[e] = T::pack4(v);
         }
-        *(u16x4*)(o + ct * 16) = T::pack4(v);
+        *(u16x8*)(o + hh * 32) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
       }
     }
   }
@@ -1337,7 +1350,7 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
   if (pw_on && !split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
       d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->cin == 64 || d->cin == 128 || (d->cin == 256 && pw256)) &&
       k_pad == d->cin &&
-      d->cout % 64 == 0 && d->ldo % 4 == 0 && d->c_off % 4 == 0 && !(d->flags & FAC_CONV_OUT_F32) &&
+      d->cout % 64 == 0 && d->ldo % 8 == 0 && d->c_off % 8 == 0 && !(d->flags & FAC_CONV_OUT_F32) &&
       (!(d->flags & FAC_CONV_RESID) || (d->ldr % 8 == 0 && d->r_off % 8 == 0))) {
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
