@@ -662,8 +662,9 @@ __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, fl
 // whole weight in LDS and walks output boxes of 8 x 28 positions: per box
 // the (11 x 31)-cell halo (2 x 16-byte channel pieces per cell) is copied to
 // LDS once and all 16 taps read it.  MFMAs run transposed (C^T = W . X^T:
-// rows = channels), so each lane ends with 4 consecutive channels of one
-// position and the epilogue stores 8 bytes straight from registers.
+// rows = channels), so each lane ends with 8 consecutive channels of one
+// position (channel-permuted tiles, below) and the epilogue stores 16 bytes
+// straight from registers.
 // k-step s covers taps 2s, 2s+1 (ty = s/2, tx = 2(s%2) + g/2) x 16 channels:
 // lane group g reads channel piece g%2 of tap 2s + g/2, i.e. k = 32s + 8g + e,
 // the natural fac_conv_nd weight order.
@@ -683,17 +684,21 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
   const int wm = wave >> 1, wn = wave & 1;
 
   // weights [s][ct][g][r16][8]: the A fragment of (k-step s, channel tile ct)
-  // is one contiguous, conflict-free 1 KB read
+  // is one contiguous, conflict-free 1 KB read.  Row i of the wave's tile ct
+  // (tiles 2wn, 2wn+1) computes channel 32 wn + 8 (i >> 2) + 4 ct + (i & 3), so
+  // lane group g ends with channels 32wn + 8g .. +7 of its position: one
+  // 16-byte store, 64 contiguous bytes per position per store instruction
   for (int c = tid; c < 64 * 32; c += 256) {
     const int n = c >> 5, k8 = c & 31;
-    *(u16x8*)(sw + ((((k8 >> 2) * 4 + (n >> 4)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+    const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
+    *(u16x8*)(sw + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) =
         *(const u16x8*)(w + (size_t)n * kp + k8 * 8);
   }
   float bv[2][4];
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[(2 * wn + ct) * 16 + 4 * g + j] : 0.f;
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[32 * wn + 8 * g + 4 * ct + j] : 0.f;
   // this lane's halo slot offsets (16-byte units) for pixel tile i at tap (0, g/2)
   int bo[7];
 #pragma unroll
@@ -734,14 +739,16 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
       const int m = (wm * 7 + i) * 16 + r16, py = m / TW, px = m - (m / TW) * TW;
-      uint16_t* o = out + (((size_t)img * Ho + y0 + py) * Wo + x0 + px) * 64 + 4 * g;
+      uint16_t* o = out + (((size_t)img * Ho + y0 + py) * Wo + x0 + px) * 64 + 32 * wn + 8 * g;
+      u16x4 q[2];
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         f32x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = relu_on ? relu(acc[i][ct][j] + bv[ct][j]) : acc[i][ct][j] + bv[ct][j];
-        *(u16x4*)(o + (2 * wn + ct) * 16) = T::pack4(v);
+        q[ct] = T::pack4(v);
       }
+      *(u16x8*)o = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
     }
   }
 }
