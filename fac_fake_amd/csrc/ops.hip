@@ -1021,16 +1021,17 @@ __global__ __launch_bounds__(512, 1) void conv_tk(const uint16_t* __restrict__ i
 // frame z (Do == 8) for the unit's 16 positions x the workgroup's 64
 // channels, MFMAs transposed as in conv_tk; the nbk column blocks of a unit
 // slot are 8 workgroup ids apart (see conv_tk).
-// vmcnt(BASE + 4k) for the wave-uniform k in 0..K (s_waitcnt takes an immediate)
-template <int BASE, int K>
+// vmcnt(BASE + ST*k) + barrier for the wave-uniform k in 0..K (s_waitcnt
+// takes an immediate): ST = stores per store batch
+template <int BASE, int K, int ST>
 __device__ __forceinline__ void wait_vm_stores(int k) {
   if constexpr (K > 0) {
     if (k < K) {
-      wait_vm_stores<BASE, K - 1>(k);
+      wait_vm_stores<BASE, K - 1, ST>(k);
       return;
     }
   }
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(BASE + 4 * K) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(BASE + ST * K) : "memory");
 }
 
 #ifdef TK2_STAMPS
@@ -1110,9 +1111,13 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
   // weight block [k-step t*CH + c][ct][g][r16][8] and biases to LDS (global
   // loads retired here, before the first glds: the loop's counted waits then
   // see only slice pieces and output stores)
+  // (row i of the wave's tile cc -- tiles 2h, 2h+1 -- computes channel
+  // 32h + 8 (i >> 2) + 4 cc + (i & 3): lane group g ends with channels
+  // 32h + 8g .. +7 of its position, one 16-byte store per output frame)
   for (int c = tid; c < 64 * KS * 4; c += 512) {
     const int n = c / (KS * 4), k8 = c - n * (KS * 4);
-    *(u16x8*)(wts + ((((k8 >> 2) * 4 + (n >> 4)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+    const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
+    *(u16x8*)(wts + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) =
         *(const u16x8*)(w + (size_t)(nb * 64 + n) * kp + k8 * 8);
   }
   if (tid < 64) bsm[tid] = bias ? bias[nb * 64 + tid] : 0.f;
@@ -1121,7 +1126,7 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
   const int fp = wave & 3, h = wave >> 2;
   f32x4 bv[2];
 #pragma unroll
-  for (int cc = 0; cc < 2; ++cc) bv[cc] = *(const f32x4*)(bsm + h * 32 + cc * 16 + 4 * g);
+  for (int cc = 0; cc < 2; ++cc) bv[cc] = *(const f32x4*)(bsm + h * 32 + 8 * g + 4 * cc);
 #pragma unroll
   for (int i = 0; i < R - 1; ++i) issue();
   const int d0 = 2 * fp * SD - PD;  // input frame of frame 2fp's tap 0
@@ -1135,11 +1140,11 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
   unsigned hist = 0;
   int cs = 0, cu = slot;  // compute cursor: step within the unit, unit
   for (int s = 0; s < nsteps; ++s) {
-    // slice s landed: younger than it are slices s+1 .. s+R-2 and the output
-    // stores of steps s-R+1 .. s-1; every wave is done with slice s-1's slot,
+    // slice s landed: younger than it are slices s+1 .. s+R-2 and the 2
+    // output stores of each unit-ending step in s-R+1 .. s-1; every wave is done with slice s-1's slot,
     // which this step's issue refills
     TK2_STAMP(0);
-    wait_vm_stores<(R - 2) * NP, R - 1>(__builtin_popcount(hist & ((1u << (R - 1)) - 1)));
+    wait_vm_stores<(R - 2) * NP, R - 1, 2>(__builtin_popcount(hist & ((1u << (R - 1)) - 1)));
     TK2_STAMP(1);
     issue();  // slice s + R - 1
     TK2_STAMP(2);
@@ -1179,14 +1184,16 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
       if (p0 + r16 < S) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          uint16_t* o = out + (((size_t)n * 8 + 2 * fp + j) * S + p0 + r16) * ldo + c_off + nb * 64 + h * 32 + 4 * g;
+          uint16_t* o = out + (((size_t)n * 8 + 2 * fp + j) * S + p0 + r16) * ldo + c_off + nb * 64 + h * 32 + 8 * g;
+          u16x4 q2[2];
 #pragma unroll
           for (int cc = 0; cc < 2; ++cc) {
             f32x4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = relu_on ? relu(acc[j][cc][q] + bv[cc][q]) : acc[j][cc][q] + bv[cc][q];
-            *(u16x4*)(o + cc * 16) = T::pack4(v);
+            q2[cc] = T::pack4(v);
           }
+          *(u16x8*)o = __builtin_shufflevector(q2[0], q2[1], 0, 1, 2, 3, 4, 5, 6, 7);
         }
       }
 #pragma unroll
