@@ -193,17 +193,21 @@ class ResVitKan(nn.Module):
             self._side = st
         return st
 
-    def features16(self, x16: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    def features16(self, x16: torch.Tensor, out: torch.Tensor | None = None, taps: list | None = None) -> torch.Tensor:
         """ResNet.forward (ResVitKan.py:232-247) on space-to-depth packed 16-bit
         cells [B,1,115,115,16] (ops.pack_input_s2d) -> [B,1,7,7,512] 16-bit
-        NHWC, in chunks of ``feature_chunk`` crops."""
+        NHWC, in chunks of ``feature_chunk`` crops.  With `taps` (one chunk
+        only): the max-pool output, every Bottleneck's output and the bn2
+        output, [B,1,H,W,C] 16-bit, are appended to it."""
         B = x16.shape[0]
         if out is None:
             out = torch.empty(B, 1, 7, 7, 512, dtype=x16.dtype, device=x16.device)
-        step = self.feature_chunk or B
+        step = B if taps is not None else (self.feature_chunk or B)
+        tap = taps.append if taps is not None else (lambda t: None)
         for b0 in range(0, B, step):
             x = self._conv1(x16[b0:b0 + step])                      # 7x7/2 + bn1 + ReLU, on s2d cells
             x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))    # MaxPool2d(3, 2, 1)
+            tap(x)
             for c1, c2, c3, ds in self._blocks:
                 if ds is not None:
                     # the downsample branch (first block of each layer) runs on a
@@ -219,8 +223,24 @@ class ResVitKan(nn.Module):
                     res = x
                     h = c2(c1(x))
                 x = c3(h, residual=res, relu2=True)                 # relu(bn3) + residual, relu
+                tap(x)
             self._channel(x, relu=False, out=out[b0:b0 + step])     # channel 1x1 + bn2
+            tap(out[b0:b0 + step])
         return out
+
+    def stage_outputs(self, crops: torch.Tensor) -> list:
+        """For uint8 crops [B,224,224,3]: the ResNet-50 outputs a forward hook on
+        the reference's ``features.maxpool``, each ``features.layerN[b]`` and
+        ``features.bn2`` sees (18 tensors, NHWC 16-bit), for per-block parity."""
+        if crops.dtype != torch.uint8 or crops.dim() != 4 or tuple(crops.shape[1:]) != (224, 224, 3):
+            raise ValueError(f"expected uint8 crops [B,224,224,3], got {crops.dtype} {tuple(crops.shape)}")
+        if not crops.is_cuda:
+            raise RuntimeError("ResVitKan (gfx950 HIP path) needs its input on a GPU device; there is no CPU fallback")
+        self._prepare(crops.device)
+        x16 = pack_input_s2d(crops, dtype=self.dtype_name, u8=True, div=255.0, mean=MEAN, std=STD)
+        taps = []
+        self.features16(x16, taps=taps)
+        return taps
 
     def _run(self, x16: torch.Tensor, pos_index, want_probs: bool):
         B = x16.shape[0]

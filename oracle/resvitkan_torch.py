@@ -47,10 +47,15 @@ def _bn(sd, p, h):
 
 
 @torch.no_grad()
-def resnet50_fp32(sd, img: torch.Tensor) -> torch.Tensor:
+def resnet50_fp32(sd, img: torch.Tensor, taps: list | None = None) -> torch.Tensor:
+    """With `taps`: the max-pool output, every Bottleneck's output and the
+    bn2 output are appended (what forward hooks on the reference's maxpool,
+    layerN[b] and bn2 see)."""
     sd = to_torch_sd(sd)
+    tap = taps.append if taps is not None else (lambda t: None)
     x = F.relu(_bn(sd, "features.bn1", F.conv2d(img.float(), sd["features.conv1.weight"], stride=2, padding=3)))
     x = F.max_pool2d(x, 3, 2, 1)
+    tap(x)
     for p, s, ds in blocks():
         res = x
         out = F.relu(_bn(sd, p + ".bn1", F.conv2d(x, sd[p + ".conv1.weight"])))
@@ -59,7 +64,10 @@ def resnet50_fp32(sd, img: torch.Tensor) -> torch.Tensor:
         if ds:
             res = _bn(sd, p + ".downsample.1", F.conv2d(x, sd[p + ".downsample.0.weight"], stride=s))
         x = F.relu(out + res)
-    return _bn(sd, "features.bn2", F.conv2d(x, sd["features.channel.weight"]))
+        tap(x)
+    y = _bn(sd, "features.bn2", F.conv2d(x, sd["features.channel.weight"]))
+    tap(y)
+    return y
 
 
 def b_splines(x: torch.Tensor, grid: torch.Tensor, order: int = 3) -> torch.Tensor:
@@ -109,9 +117,11 @@ def fold_bn(sd, conv_key: str, bn_prefix: str):
 
 
 @torch.no_grad()
-def resnet50_emulated(sd, img: torch.Tensor, dtype: str = "bf16") -> torch.Tensor:
-    """ResNet-50 stem at the HIP path's rounding points (fac_conv_nd epilogues)."""
+def resnet50_emulated(sd, img: torch.Tensor, dtype: str = "bf16", taps: list | None = None) -> torch.Tensor:
+    """ResNet-50 stem at the HIP path's rounding points (fac_conv_nd epilogues);
+    `taps` as in resnet50_fp32."""
     sd = to_torch_sd(sd)
+    tap = taps.append if taps is not None else (lambda t: None)
     r = lambda t: round_to(t, dtype)  # noqa: E731
 
     def conv(x, ck, bnp, stride=1, pad=0, relu=True, res=None):
@@ -125,12 +135,16 @@ def resnet50_emulated(sd, img: torch.Tensor, dtype: str = "bf16") -> torch.Tenso
 
     x = conv(r(img.float()), "features.conv1.weight", "features.bn1", 2, 3)
     x = F.max_pool2d(x, 3, 2, 1)
+    tap(x)
     for p, s, ds in blocks():
         res = conv(x, p + ".downsample.0.weight", p + ".downsample.1", s, 0, relu=False) if ds else x
         out = conv(x, p + ".conv1.weight", p + ".bn1")
         out = conv(out, p + ".conv2.weight", p + ".bn2", s, 1)
         x = conv(out, p + ".conv3.weight", p + ".bn3", res=res)
-    return conv(x, "features.channel.weight", "features.bn2", relu=False)
+        tap(x)
+    y = conv(x, "features.channel.weight", "features.bn2", relu=False)
+    tap(y)
+    return y
 
 
 @torch.no_grad()

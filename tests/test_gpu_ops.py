@@ -226,6 +226,33 @@ def test_resvitkan_matches_reference(rvk, golden, dt, tol):
         assert np.abs(p - p_ref).max() <= tol
 
 
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_resvitkan_every_block_matches_reference(rvk, golden, dt):
+    """8 crops: the per-channel means of the max-pool output, of EVERY Bottleneck
+    (layer1..layer4, downsample and residual included) and of bn2 against the
+    reference module's (tests/golden/resvitkan_golden_stages.npz), within 2x
+    that stage's emulated 16-bit envelope; probabilities fp16 within 1e-3,
+    bf16 within 2x its emulated envelope."""
+    g = golden("resvitkan_golden_stages.npz")
+    n = int(g["n_crops"])
+    x = torch.from_numpy(make_crops(n, seed=int(g["crop_seed"]))).to(DEV)
+    m = rvk[dt]
+    taps = m.stage_outputs(x)
+    torch.cuda.synchronize()
+    assert len(taps) == 18
+    env = g[f"env_{dt}"]
+    for i, t in enumerate(taps):
+        got = t.float().reshape(n, -1, t.shape[-1]).mean(1).double().cpu().numpy()
+        ref = g[f"mean_{i}"].astype(np.float64)
+        assert got.shape == ref.shape, (i, got.shape, ref.shape)
+        err = float(np.abs(got - ref).max() / np.sqrt((ref ** 2).mean()))
+        assert err <= 2 * env[i] + 1e-4, (i, err, env[i])
+    lg, pr = m.forward_u8(x, pos_index=torch.arange(n, dtype=torch.int32), return_probs=True)
+    p_ref = 1 / (1 + np.exp(-g["logits"].astype(np.float64)))
+    bar = 1e-3 if dt == "fp16" else 2 * float(g[f"env_prob_{dt}"])
+    assert np.abs(pr.double().cpu().numpy() - p_ref).max() <= bar
+
+
 def test_resvitkan_features_match_emulation(rvk, golden):
     """The ResNet-50 stem alone vs the oracle's emulation of the same 16-bit
     rounding points (fp16): relative error of the [B,7,7,512] features."""

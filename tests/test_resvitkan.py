@@ -66,3 +66,19 @@ def test_b_splines_partition_of_unity():
     x = torch.linspace(-0.99, 0.99, 40).view(10, 4)
     s = b_splines(x, g).sum(-1)
     assert torch.allclose(s, torch.ones_like(s), atol=1e-6)
+
+
+def test_oracle_every_block_matches_reference(golden, torch_threads):
+    """The oracle's max-pool, 16 Bottleneck and bn2 outputs on 8 crops: per-channel
+    means equal to the reference module's (resvitkan_golden_stages.npz)."""
+    from oracle import resvitkan_torch as O
+    from oracle.cvit_torch import normalize_u8, to_torch_sd
+    g = golden("resvitkan_golden_stages.npz")
+    x = normalize_u8(make_crops(int(g["n_crops"]), seed=int(g["crop_seed"])))
+    taps = []
+    O.resnet50_fp32(to_torch_sd(make_resvitkan_state_dict(0)), x, taps)
+    assert len(taps) == 18
+    for i, t in enumerate(taps):
+        got = t.double().mean(dim=(2, 3)).numpy()
+        ref = g[f"mean_{i}"].astype(np.float64)
+        assert np.abs(got - ref).max() <= 1e-5 * np.sqrt((ref ** 2).mean()) + 1e-7, i

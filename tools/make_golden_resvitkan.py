@@ -12,6 +12,13 @@ seed 0) and records the reference's outputs.  Data only, no reference source:
                         and hidden-layer checksums, KAN layer-0 outputs, logits;
                         a KANLinear(2048, 64) on inputs spanning the whole
                         grid and beyond (seed 22): inputs and outputs
+  resvitkan_golden_stages.npz
+                        8 crops (make_crops seed 43, slots 0..7): logits and,
+                        for the max-pool, each of the 16 Bottlenecks and bn2,
+                        the per-channel mean over (H, W) of its output, plus
+                        the 16-bit rounding envelope of each (the oracle's
+                        emulation of the HIP path's rounding points vs the
+                        reference), so a GPU test can localise a wrong block
 """
 from __future__ import annotations
 
@@ -68,6 +75,42 @@ def main():
         kan0=kan0["k"].numpy(), kan_x=kx.numpy(), kan_y=ky.numpy())
     print("logits", logits.numpy())
     print("feat range", f.min(), f.max(), "hidden range", h.min(), h.max())
+    stages(m, sd)
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / (np.sqrt((b.astype(np.float64) ** 2).mean()) + 1e-30))
+
+
+def stages(m, sd):
+    from oracle import resvitkan_torch as O  # the rounding-point emulation, for the envelope only
+    from oracle.cvit_torch import to_torch_sd
+    seed, n = 43, 8
+    x = ref_normalize(make_crops(n, seed=seed))
+    taps = []
+    f = m.features
+    mods = [f.maxpool] + [blk for layer in (f.layer1, f.layer2, f.layer3, f.layer4) for blk in layer] + [f.bn2]
+    hooks = [md.register_forward_hook(lambda mod, i, o: taps.append(o.detach().clone())) for md in mods]
+    with torch.no_grad():
+        logits = m(x).numpy()
+    for hk in hooks:
+        hk.remove()
+    assert len(taps) == 18
+    means = [t.double().mean(dim=(2, 3)).numpy() for t in taps]
+    out = {"crop_seed": np.int64(seed), "n_crops": np.int64(n), "logits": logits}
+    for i, mu in enumerate(means):
+        out[f"mean_{i}"] = mu.astype(np.float32)
+    tsd = to_torch_sd(sd)
+    p_ref = 1 / (1 + np.exp(-logits.astype(np.float64)))
+    for dt in ("fp16", "bf16"):
+        et = []
+        O.resnet50_emulated(tsd, x, dt, et)
+        out[f"env_{dt}"] = np.array([_rel(t.double().mean(dim=(2, 3)).numpy(), mu) for t, mu in zip(et, means)])
+        pe = torch.sigmoid(O.forward_emulated(tsd, x, dtype=dt)).double().numpy()
+        out[f"env_prob_{dt}"] = np.float64(np.abs(pe - p_ref).max())
+        print(dt, "env", np.round(out[f"env_{dt}"], 4), "prob", out[f"env_prob_{dt}"])
+    print("probs", np.round(p_ref, 4))
+    np.savez_compressed(OUT / "resvitkan_golden_stages.npz", **out)
 
 
 if __name__ == "__main__":
