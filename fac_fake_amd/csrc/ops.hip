@@ -364,14 +364,21 @@ __global__ __launch_bounds__(256) void pool_nd(fac_pool_desc p, int total) {
 // the frame max over a sliding window of three, so the map is read from HBM
 // about once and written once — one pass instead of the separable version's
 // three, bit-identical (a max selects one of its inputs either way).
+// zg: output frames per thread (all of them by default).  Round 3 tried
+// 1 / 2 / 4 of S3D's 8 frames per thread for more parallelism: the whole
+// S3D step got 9 / 4 / 1 % slower (same box, tools/pool_ab.sh): the frame
+// walk's reuse of the frame maxima, not latency, is what counts.
 template <class T>
-__global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total) {
+__global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total, int zg) {
   const int t = blockIdx.x * 256 + threadIdx.x;
   if (t >= total) return;
   const int C8 = p.c / 8;
   const int c8 = t % C8, t1 = t / C8;
   const int x = t1 % p.w, t2 = t1 / p.w;
-  const int y = t2 % p.h, n = t2 / p.h;
+  const int y = t2 % p.h, t3 = t2 / p.h;
+  const int ngr = (p.d + zg - 1) / zg;
+  const int zgi = t3 % ngr, n = t3 / ngr;
+  const int z0 = zgi * zg, z1 = min(p.d, z0 + zg);
   const size_t fs = (size_t)p.h * p.w * p.c;
   const uint16_t* inb = (const uint16_t*)p.in + (size_t)n * p.d * fs + c8 * 8;
   auto frame_max = [&](int z, float (&m)[8]) {
@@ -393,11 +400,15 @@ __global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total) {
     }
   };
   float pm[8], cm[8], nm[8];
+  if (z0 > 0) {
+    frame_max(z0 - 1, pm);
+  } else {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) pm[i] = -__builtin_inff();
-  frame_max(0, cm);
+    for (int i = 0; i < 8; ++i) pm[i] = -__builtin_inff();
+  }
+  frame_max(z0, cm);
   uint16_t* ob = (uint16_t*)p.out + ((size_t)n * p.d * p.h * p.w + (size_t)y * p.w + x) * p.ldo + p.c_off + c8 * 8;
-  for (int z = 0; z < p.d; ++z) {
+  for (int z = z0; z < z1; ++z) {
     if (z + 1 < p.d) {
       frame_max(z + 1, nm);
     } else {
@@ -1509,12 +1520,18 @@ int fac_pool_nd(const fac_pool_desc* d, void* stream) {
   }();
   if (mp3 && d->mode == 0 && d->kd == 3 && d->kh == 3 && d->kw == 3 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
       d->pd == 1 && d->ph == 1 && d->pw == 1 && d->od == d->d && d->oh == d->h && d->ow == d->w) {
-    const long long cols = (long long)d->n * d->h * d->w * (d->c / 8);  // one thread walks the frames
+    static const int zg_env = [] {  // output frames per thread (FAC_POOL_ZG; default: all of them)
+      const char* e = std::getenv("FAC_POOL_ZG");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int zg = zg_env > 0 ? zg_env : d->d;
+    const long long cols = (long long)d->n * ((d->d + zg - 1) / zg) * d->h * d->w * (d->c / 8);
+    if (cols >= (1LL << 31)) return FAC_ERR_SHAPE;
     const int nb = (int)((cols + 255) / 256);
     if (d->dtype == FAC_DTYPE_BF16)
-      maxpool3_s1<BF16><<<nb, 256, 0, st>>>(*d, (int)cols);
+      maxpool3_s1<BF16><<<nb, 256, 0, st>>>(*d, (int)cols, zg);
     else
-      maxpool3_s1<F16><<<nb, 256, 0, st>>>(*d, (int)cols);
+      maxpool3_s1<F16><<<nb, 256, 0, st>>>(*d, (int)cols, zg);
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   const int nb = (int)((total + 255) / 256);
