@@ -137,7 +137,7 @@ struct fac_ctx {
   int* errflag = nullptr;      // device view
   int* err_host = nullptr;     // host view of the same int
   int* sched = nullptr;  // 2 ints: stem224 dynamic box counter + finished-workgroup count
-  int stem_dynamic = 1;  // option "stem_dynamic": stem224 claims boxes from `sched` (else static)
+  int stem_dynamic = 0;  // option "stem_dynamic": stem224 claims boxes from `sched` (default: static, no atomics)
   int stem_nwg = 0;      // option "stem_nwg": persistent stem workgroups (0 = one per CU)
   // option "stem_events": hipEvent pairs around every fused-stem launch (the
   // bench's timed region), read back by fac_stem_event_ms

@@ -53,9 +53,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // img + rd[i]: tile i's fragment for tap 0; tap (ky,kx) is ky*RP + kx pixel
 // slots further.  wl: this lane's weight row; tap t, channel tile ct at
 // wl + (t*128 + ct*16)*8 (weights [tap][q][32][8]).
-template <class T, bool TR, int NT, int RP>
+// mid(): work issued inside tap 2's MFMA stream (its VALU then issues in the
+// MFMAs' shadow instead of ahead of the taps).
+template <class T, bool TR, int NT, int RP, class Mid>
 __device__ __forceinline__ void tap_pipeline(f32x4 (&acc)[NT][2], const uint16_t* img, const int (&rd)[NT],
-                                             const uint16_t* wl) {
+                                             const uint16_t* wl, Mid&& mid) {
   u16x8 fa[NT], wf[2];
 #pragma unroll
   for (int i = 0; i < NT; ++i) fa[i] = *(const u16x8*)(img + rd[i]);
@@ -69,6 +71,7 @@ __device__ __forceinline__ void tap_pipeline(f32x4 (&acc)[NT][2], const uint16_t
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) wn[ct] = *(const u16x8*)(wl + ((t + 1) * 128 + ct * 16) * 8);
     }
+    if (t == 2) mid();
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
 #pragma unroll
@@ -110,7 +113,9 @@ __device__ unsigned long long stem_st[4][32][8][8];
   } while (0)
 #endif
 
-template <class T, bool U8>
+// DYN: boxes claimed from a global counter (see below); false: static
+// schedule with no atomic compiled in
+template <class T, bool U8, bool DYN>
 __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__ in_,
                                                         const uint16_t* __restrict__ w1g,
                                                         const float* __restrict__ b1,
@@ -119,7 +124,8 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
                                                         const uint16_t* __restrict__ w3g,
                                                         const float* __restrict__ b3,
                                                         uint16_t* __restrict__ out, int ntiles,
-                                                        int* __restrict__ sched) {
+                                                        int* __restrict__ sched_) {
+  int* const sched = DYN ? sched_ : nullptr;      // compile-time null: no atomic, no claim register
   constexpr int IMG = 224, TPR = 7, TPI = 98;     // 16x32 boxes per box row / per image
   constexpr int BW = 32;                          // box width (height 16)
   constexpr int IW = BW + 6, IN_PIX = 22 * IW;    // input region 22 x 38
@@ -219,9 +225,48 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   uint32_t raw01[2], raw2[2];  // U8: channels 0|1 (one 2-byte load), channel 2
   float raw[2][3];
   bool raw_in[2];
+  // Round 3: the U8 loads are unconditional (out-of-image and past-the-end
+  // pixels read a valid pixel that is then discarded), all four issued back to back.  The branchy
+  // form made the compiler re-allocate a pending load's registers and put
+  // `s_waitcnt vmcnt(0)` between the two pixel pairs (every wave waited for
+  // the first pair's HBM round trip, and for its own previous output stores:
+  // 600-1400 cycles per box, tools/ubench/stem_ubench.hip stamp 8).
+  // this thread's two receptive-field pixels (row, column, byte offset
+  // within the box's window), fixed for every box
+  int f_iy[2], f_ix[2], f_off[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = tid + 512 * k;
+    f_iy[k] = p < IN_PIX ? p / IW : 1 << 20;  // past the window: never in the image
+    f_ix[k] = p - (p / IW) * IW;
+    f_off[k] = (f_iy[k] * IMG + f_ix[k]) * 3;
+  }
   auto fetch = [&](int tile) {
     const int b = tile / TPI, rr = tile - (tile / TPI) * TPI;
     const int ty = rr / TPR, tx = rr - (rr / TPR) * TPR;
+    if constexpr (U8) {
+      // window origin (ty*16 - 3, tx*BW - 3) of crop b: wave-uniform
+      const int oy = ty * 16 - 3, ox = tx * BW - 3;
+      const long long wbase = ((long long)b * IMG * IMG + oy * IMG + ox) * 3;  // < 0 only for crop 0's top-left box
+      const uint8_t* src[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        raw_in[k] = tile < ntiles && (unsigned)(oy + f_iy[k]) < (unsigned)IMG && (unsigned)(ox + f_ix[k]) < (unsigned)IMG;
+        // out-of-image / past-the-end pixels load a valid pixel (crop 0's
+        // first) whose value phase A discards (raw_in); one address space,
+        // so the loads stay global_load (a select with another array made
+        // them flat loads, which need vmcnt(0) lgkmcnt(0) waits)
+        src[k] = (const uint8_t*)in_ + (raw_in[k] ? wbase + f_off[k] : 0LL);
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        uint16_t v01;
+        __builtin_memcpy(&v01, src[k], 2);
+        raw01[k] = v01;
+        raw2[k] = src[k][2];
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       raw01[k] = raw2[k] = 0;
@@ -234,11 +279,6 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       if (y < 0 || y >= IMG || x < 0 || x >= IMG) continue;
       raw_in[k] = true;
       if constexpr (U8) {
-        const uint8_t* src = (const uint8_t*)in_ + (((size_t)b * IMG + y) * IMG + x) * 3;
-        uint16_t v01;
-        __builtin_memcpy(&v01, src, 2);
-        raw01[k] = v01;
-        raw2[k] = src[2];
       } else {
         const float* src = (const float*)in_ + (size_t)b * 3 * IMG * IMG + (size_t)y * IMG + x;
         raw[k][0] = src[0];
@@ -262,6 +302,9 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
   if (sched) tile = s_tile[0];
   fetch(tile);
 
+  bool pend = false;  // a pooled tile waiting to be stored
+  uint16_t* pend_ptr = out;
+  u16x8 pend_v = (u16x8)0;
   for (int j = 0; tile < ntiles; ++j) {
     // the claim's round trip overlaps staging and conv1: it is published in
     // LDS only before conv1's closing barrier
@@ -290,6 +333,13 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
       h[3] = 0;
       hv[k] = h;
     }
+    // the previous box's pooled tile leaves here, after this box's pixel
+    // loads were consumed: at the loop head those loads are then the
+    // youngest memory operations on every path, so their wait is exact and
+    // never waits for a just-issued output store (storing at the end of the
+    // box put the store behind the loads, and the compiler's merged wait for
+    // the first and later iterations then drained the store too)
+    if (pend) *(u16x8*)pend_ptr = pend_v;
     lds_barrier();  // previous tile's readers of sin(=c2) and ostg(=c1) are done
     STEM_STAMP(0);
 #pragma unroll
@@ -363,7 +413,6 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     STEM_STAMP(2);
 
     const int next = sched ? s_tile[(j + 1) & 1] : tile + gridDim.x;
-    fetch(next);  // next box's pixels land while conv2/conv3 run
 
     // ---- C: conv2 over the 18x34 region at (y0-1, x0-1): window-major, 39 row tiles
     // (wave 7's fifth tile is a dummy over pixel 0, computed and not stored:
@@ -376,7 +425,8 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         acc[i][0] = bt2[0];
         acc[i][1] = bt2[1];
       }
-      tap_pipeline<T, true, N2, RP>(acc, c1, c2_rd, sw2 + (g * 32 + r16) * 8);
+      // the next box's pixels are fetched inside conv2's taps and land while conv2/conv3 run
+      tap_pipeline<T, true, N2, RP>(acc, c1, c2_rd, sw2 + (g * 32 + r16) * 8, [&] { fetch(next); });
       STEM_STAMP(5);
 #pragma unroll
       for (int i = 0; i < N2; ++i) {
@@ -409,7 +459,7 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
         acc[i][0] = bn3[0];
         acc[i][1] = bn3[1];
       }
-      tap_pipeline<T, false, 4, RP>(acc, c2, c3_rd, sw3 + (g * 32 + r16) * 8);
+      tap_pipeline<T, false, 4, RP>(acc, c2, c3_rd, sw3 + (g * 32 + r16) * 8, [] {});
       STEM_STAMP(6);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -422,14 +472,18 @@ __global__ __launch_bounds__(512, 1) void stem224_fused(const void* __restrict__
     }
     lds_barrier();
     STEM_STAMP(4);
-    {  // 128 pooled pixels x 4 16-byte channel quarters = 512 threads
+    {  // 128 pooled pixels x 4 16-byte channel quarters = 512 threads: read
+       // now (ostg is overwritten in the next box's phase B), stored after
+       // the next box's staging
       const int w = tid >> 2, q = tid & 3;
       const int wy = w >> 4, wx = w & 15;
-      *(u16x8*)(out + (((size_t)b * 112 + (y0 >> 1) + wy) * 112 + (x0 >> 1) + wx) * 32 + q * 8) =
-          *(const u16x8*)(ostg + w * 40 + q * 8);
+      pend_ptr = out + (((size_t)b * 112 + (y0 >> 1) + wy) * 112 + (x0 >> 1) + wx) * 32 + q * 8;
+      pend_v = *(const u16x8*)(ostg + w * 40 + q * 8);
+      pend = true;
     }
     tile = next;
   }
+  if (pend) *(u16x8*)pend_ptr = pend_v;
   // every claim of every workgroup precedes its arrival here: the last one
   // to arrive leaves both counters at zero for the next launch
   if (sched && tid == 0 && atomicAdd(sched + 1, 1) == (int)gridDim.x - 1) {
@@ -443,13 +497,15 @@ hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1
                           hipStream_t st, int* sched) {
   const int ntiles = B * 98;  // 16x32 boxes
   const int grid = nwg < ntiles ? nwg : ntiles;
+#define FAC_STEM(TT, U, D) stem224_fused<TT, U, D><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched)
   if (dtype == 0) {
-    if (u8) stem224_fused<BF16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
-    else stem224_fused<BF16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
+    if (sched) u8 ? FAC_STEM(BF16, true, true) : FAC_STEM(BF16, false, true);
+    else u8 ? FAC_STEM(BF16, true, false) : FAC_STEM(BF16, false, false);
   } else {
-    if (u8) stem224_fused<F16, true><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
-    else stem224_fused<F16, false><<<grid, 512, 0, st>>>(in, w1, b1, w2, b2, w3, b3, out, ntiles, sched);
+    if (sched) u8 ? FAC_STEM(F16, true, true) : FAC_STEM(F16, false, true);
+    else u8 ? FAC_STEM(F16, true, false) : FAC_STEM(F16, false, false);
   }
+#undef FAC_STEM
   return hipGetLastError();
 }
 
