@@ -680,16 +680,16 @@ __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, fl
 // lane group g reads channel piece g%2 of tap 2s + g/2, i.e. k = 32s + 8g + e,
 // the natural fac_conv_nd weight order.
 template <class T>
-__global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+__global__ __launch_bounds__(256, 2) void conv_s2d4(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
                                                     const float* __restrict__ bias, uint16_t* __restrict__ out,
                                                     int nbox, int Hc, int Wc, int Ho, int Wo, int kp, int relu_on) {
   constexpr int TH = 8, TW = 28, HH = TH + 3, HWD = TW + 3, RPX = 32;  // halo rows, cols, row pitch (cells)
   constexpr int HSL = 2 * HH * RPX;                                       // 16-byte halo slots
   constexpr int HPW = (HSL + 255) / 256;                                  // glds per wave
   constexpr int WEL = 64 * 256;                                           // weight elements
-  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + HPW * 256 * 8];
+  constexpr int HEL = HPW * 256 * 8;                                     // halo buffer elements
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * HEL];
   uint16_t* const sw = smem;
-  uint16_t* const halo = smem + WEL;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int wm = wave >> 1, wn = wave & 1;
@@ -718,10 +718,14 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
     bo[i] = ((g & 1) * HH + py) * RPX + px + (g >> 1);
   }
   const int bpr = Wo / TW, bpi = (Ho / TH) * bpr;
-  for (int bx = blockIdx.x; bx < nbox; bx += gridDim.x) {
+  // Round 3: the halo is double-buffered (the next box's streams in while this
+  // one computes), and the wait for a box's halo counts the previous box's 7
+  // output stores per lane as younger operations: vmcnt counts loads and
+  // stores in issue order, so `__syncthreads()` / `vmcnt(0)` per box also
+  // waited for the previous box's stores to reach HBM.
+  auto issue = [&](int bx, uint16_t* halo) {
     const int img = bx / bpi, rr = bx - img * bpi;
     const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
-    __syncthreads();  // the previous box's halo reads are done (and, first time, the weights are in)
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
       const int sl = (i * 4 + wave) * 64 + lane;
@@ -730,7 +734,27 @@ __global__ __launch_bounds__(256, 3) void conv_s2d4(const uint16_t* __restrict__
       if (pc < 2 && hx < HWD) src = in + (((size_t)img * Hc + y0 + hy) * Wc + x0 + hx) * 16 + pc * 8;
       glds16(src, halo + (i * 4 + wave) * 64 * 8);
     }
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  __syncthreads();  // weights in
+  if (blockIdx.x < nbox) issue(blockIdx.x, smem + WEL);
+  int it = 0;
+  for (int bx = blockIdx.x; bx < nbox; bx += gridDim.x, ++it) {
+    const int img = bx / bpi, rr = bx - img * bpi;
+    const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
+    uint16_t* const halo = smem + WEL + (it & 1) * HEL;
+    const bool more = bx + (int)gridDim.x < nbox;
+    // every wave is done with the other buffer (the previous box): refill it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (more) issue(bx + gridDim.x, smem + WEL + ((it + 1) & 1) * HEL);
+    // this box's halo landed; younger: the next box's pieces (if any) and,
+    // after the first box, the previous box's 7 stores
+    if (it == 0) {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW + 7) : "memory");
+      else asm volatile("s_waitcnt vmcnt(7)\n\ts_barrier" ::: "memory");
+    }
     f32x4 acc[7][2];
 #pragma unroll
     for (int i = 0; i < 7; ++i) acc[i][0] = acc[i][1] = (f32x4)0.f;
@@ -848,7 +872,14 @@ __global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ i
     const int mrow = t * BM + wave * RT * 16 + r16;  // this lane's position in row tile 0
     if (t + (int)gridDim.x < ntiles) {
       issue(t + gridDim.x, buf ^ 1);  // its buffer's readers passed the previous tile's barrier
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PER + RPER) : "memory");
+      // this tile's pieces landed.  Younger than them: the next tile's pieces
+      // and (after the first tile) the previous tile's 2*RT output stores --
+      // vmcnt counts loads and stores in issue order, so a count of only the
+      // next tile's pieces also waited for those stores' HBM round trip.  The
+      // previous tile is never the partial last one (that is a workgroup's
+      // final tile), so every lane issued all of its stores.
+      if (it == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PER + RPER) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PER + RPER + 2 * RT) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -1353,7 +1384,7 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
-    const int grid = std::min(nbox, 3 * ncu);
+    const int grid = std::min(nbox, 2 * ncu);  // two resident (two halo buffers + weights: 56 KB each)
     const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
     if (d->dtype == FAC_DTYPE_BF16)
       conv_s2d4<BF16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
