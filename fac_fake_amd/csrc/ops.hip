@@ -80,13 +80,51 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                    (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
+#ifdef ND_STAMPS
+// diagnostic build only (tools/ubench/nd_ubench.hip): s_memtime stamps of
+// every wave of the first workgroups, per K step, into a buffer of their own
+__device__ unsigned long long nd_st[8][40][8][4];
+__device__ unsigned long long nd_ev[8][8][4];  // per wave: entry, prologue done, loop done, end
+#define ND_STAMP(k)                                                                          \
+  do {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    unsigned long long t_;                                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    if (blockIdx.x < 8 && lane == 0 && s < 40) nd_st[blockIdx.x][s][wave][(k)] = t_;         \
+  } while (0)
+#define ND_EV(k)                                                                             \
+  do {                                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    unsigned long long t_;                                                                   \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+    __builtin_amdgcn_sched_barrier(0);                                                       \
+    if (blockIdx.x < 8 && (threadIdx.x & 63) == 0) nd_ev[blockIdx.x][threadIdx.x >> 6][(k)] = t_; \
+  } while (0)
+#else
+#define ND_STAMP(k) \
+  do {              \
+  } while (0)
+#define ND_EV(k) \
+  do {           \
+  } while (0)
+#endif
+
 // UT (uniform tap): cin % 64 == 0, so every K step (64 channels) lies in one
 // tap and the tap / channel offset of a step is the same for every lane: the
 // gather is one precomputed row offset + a wave-uniform step offset per A
 // piece, validity by three unsigned compares, and no per-lane (channel piece,
 // tap) tracking or per-piece branches (the generic path's VALU work was ~8.5
 // instructions per MFMA on the ResNet-50 layers: profiles/r03_resvitkan_pmc.json).
-template <class T, int BM, int BN, int WM, int WN, int OCC, int NS, bool UT = false>
+//
+// IL (interleaved issue, UT only): the next stage's glds pieces are issued
+// one at a time between the step's MFMA groups instead of all at the step
+// start.  A CU's TA takes ~1.3k cycles for the 48 KB of a 256 x 128 stage,
+// and issued in one block by all 8 waves at once (lock-step after the
+// barrier) that time added to the ~1.1k cycles of the MFMAs (s_memtime
+// stamps, tools/ubench/nd_ubench.hip); interleaved, one wave's stalled glds
+// issue overlaps the other SIMD wave's MFMAs.
+template <class T, int BM, int BN, int WM, int WN, int OCC, int NS, bool UT = false, bool IL = false>
 __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
   constexpr int NW = WM * WN, NT = NW * 64;  // waves, threads
   constexpr int BK = 64;
@@ -102,6 +140,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
   constexpr int SMEM = OPER > STG ? OPER : STG;
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
+  ND_EV(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   int bx = blockIdx.x, by = blockIdx.y;
@@ -155,33 +194,40 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
   int uc = 0, uz = 0, uy = 0, ux = 0;
   const long long rowstride = (long long)p.W * p.C8 * 8, planestride = rowstride * p.H;
 
+  // UT: glds piece q (A pieces 0..NA-1, then B) of stage st at the step state (uz, uy, ux, uc)
+  auto ut_piece = [&](int st, int q) {
+    uint16_t* slot = smem + (st % NS) * SLOT;
+    const bool real = st < p.ksteps;
+    if (q < NA) {
+      const long long toff = uz * planestride + uy * rowstride + (long long)ux * p.C8 * 8 + uc;
+      const bool ok = real & ((unsigned)(riz[q] + uz) < (unsigned)p.D) & ((unsigned)(riy[q] + uy) < (unsigned)p.H) &
+                      ((unsigned)(rix[q] + ux) < (unsigned)p.W);
+      const uint16_t* src = ok ? p.in + (roff[q] + toff) : g_zero16;
+      glds16(src, slot + (NW * q + wave) * 64 * 8);
+    } else {
+      glds16(real ? wsrc[q - NA] + (size_t)st * BK : g_zero16, slot + SLOT_A + (NW * (q - NA) + wave) * 64 * 8);
+    }
+  };
+  auto ut_advance = [&] {
+    uc += 64;
+    if (uc == p.C8 * 8) {
+      uc = 0;
+      if (++ux == p.KW) {
+        ux = 0;
+        if (++uy == p.KH) {
+          uy = 0;
+          ++uz;
+        }
+      }
+    }
+  };
   // stage st -> ring slot st % NS; stages past the end copy zeros into slots never read
   auto issue = [&](int st) {
     uint16_t* slot = smem + (st % NS) * SLOT;
     if constexpr (UT) {
-      const bool real = st < p.ksteps;
-      const long long toff = uz * planestride + uy * rowstride + (long long)ux * p.C8 * 8 + uc;
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const bool ok = real & ((unsigned)(riz[i] + uz) < (unsigned)p.D) & ((unsigned)(riy[i] + uy) < (unsigned)p.H) &
-                        ((unsigned)(rix[i] + ux) < (unsigned)p.W);
-        const uint16_t* src = ok ? p.in + (roff[i] + toff) : g_zero16;
-        glds16(src, slot + (NW * i + wave) * 64 * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-        glds16(real ? wsrc[i] + (size_t)st * BK : g_zero16, slot + SLOT_A + (NW * i + wave) * 64 * 8);
-      uc += 64;
-      if (uc == p.C8 * 8) {
-        uc = 0;
-        if (++ux == p.KW) {
-          ux = 0;
-          if (++uy == p.KH) {
-            uy = 0;
-            ++uz;
-          }
-        }
-      }
+      for (int q = 0; q < PER; ++q) ut_piece(st, q);
+      ut_advance();
       return;
     }
     const bool real = st < p.ksteps && t.kp < p.ktot8;
@@ -210,10 +256,45 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) issue(st);
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NS - 2) * PER) : "memory");
+  ND_EV(1);
   for (int s = 0; s < p.ksteps; ++s) {
-    issue(s + NS - 1);  // into the slot consumed at step s-1 (every wave passed its barrier)
+    ND_STAMP(0);
     const uint16_t* a = smem + (s % NS) * SLOT;
     const uint16_t* b = a + SLOT_A;
+    if constexpr (IL) {
+      // stage s+NS-1 into the slot consumed at step s-1 (every wave passed its
+      // barrier), one piece after each of the first QPK MFMA groups of a K half
+      constexpr int KH = BK / 32, QPK = (PER + KH - 1) / KH;
+      static_assert(QPK <= RT, "a glds piece per MFMA group at most");
+      const int st = s + NS - 1;
+#pragma unroll
+      for (int ks = 0; ks < KH; ++ks) {
+        const int c = ks * 4 + (lane >> 4);
+        u16x8 fb[CT], fa[RT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int r = wn * WTN + ct * 16 + (lane & 15);
+          fb[ct] = *(const u16x8*)(b + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const int r = wm * WTM + rt * 16 + (lane & 15);
+          fa[rt] = *(const u16x8*)(a + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+        }
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = T::mfma(fa[rt], fb[ct], acc[rt][ct]);
+          __builtin_amdgcn_sched_barrier(0);
+          if (rt < QPK && ks * QPK + rt < PER) ut_piece(st, ks * QPK + rt);
+        }
+      }
+      ut_advance();
+      ND_STAMP(1);
+    } else {
+    issue(s + NS - 1);  // into the slot consumed at step s-1 (every wave passed its barrier)
+    ND_STAMP(1);
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       const int c = ks * 4 + (lane >> 4);
@@ -231,10 +312,19 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
         for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = T::mfma(fa, fb[ct], acc[rt][ct]);
       }
     }
+    }
     // retire stage s+1 (stage s+2 stays in flight)
+#ifdef ND_STAMPS
+    ND_STAMP(2);
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"((NS - 2) * PER) : "memory");
+    ND_STAMP(3);
+    asm volatile("s_barrier" ::: "memory");
+#else
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((NS - 2) * PER) : "memory");
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // dummy stages landed: LDS is free
+  ND_EV(2);
 
   // ---- epilogue: bias (+ReLU) in registers -> fp32 LDS tile -> 8-channel
   // vectors.  The residual's 16-byte vectors are loaded first, so their
@@ -312,6 +402,10 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
       }
     }
   }
+#ifdef ND_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  ND_EV(3);
 }
 
 // ---- pooling: one thread per (output position, 8-channel piece)
@@ -1264,28 +1358,56 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
   return dim3(gx, ny);
 }
 
-template <class T, bool UT>
+template <class T, bool UT, bool IL>
 static void launch_convnd_t(ConvP p, hipStream_t st) {
   const int gx64 = (p.M + 63) / 64, gx128 = (p.M + 127) / 128, gx256 = (p.M + 255) / 256;
   const int ny64 = (p.Cout + 63) / 64, ny128 = (p.Cout + 127) / 128;
+  // FAC_ND_TILE forces one tile (layer A/Bs: tools/nd_layers.py): 1 = 128x64
+  // (2/CU), 2 = 256x128, 3 = 128x64 2-slot (3/CU), 4 = 64x64
+  static const int force = [] {
+    const char* e = std::getenv("FAC_ND_TILE");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (force == 1 || (force == 2 && p.Cout % 128)) {
+    convnd_igemm<T, 128, 64, 2, 2, 2, 3, UT, IL><<<conv_grid(p, gx128, ny64), 256, 0, st>>>(p);
+    return;
+  }
+  if (force == 2) {
+    convnd_igemm<T, 256, 128, 4, 2, 1, 3, UT, IL><<<conv_grid(p, gx256, ny128), 512, 0, st>>>(p);
+    return;
+  }
+  if (force == 3) {
+    convnd_igemm<T, 128, 64, 2, 2, 3, 2, UT, IL><<<conv_grid(p, gx128, ny64), 256, 0, st>>>(p);
+    return;
+  }
+  if (force == 4) {
+    convnd_igemm<T, 64, 64, 2, 2, 3, 3, UT, IL><<<conv_grid(p, gx64, ny64), 256, 0, st>>>(p);
+    return;
+  }
+  static const int nd256_min = [] {
+    const char* e = std::getenv("FAC_ND256_MIN");
+    return e ? std::atoi(e) : 256;
+  }();
   if (p.ksteps <= 2) {
     // K <= 128 (1x1 expansions): memory-bound, so occupancy first — a 2-slot
     // ring (48 KB) lets three 128 x 64 workgroups share a CU
     const dim3 g = conv_grid(p, gx128, ny64);
-    convnd_igemm<T, 128, 64, 2, 2, 3, 2, UT><<<g, 256, 0, st>>>(p);
+    convnd_igemm<T, 128, 64, 2, 2, 3, 2, UT, IL><<<g, 256, 0, st>>>(p);
   } else if ((long long)gx128 * ny64 < 512) {
     // small grids (S3D's late 4x7x7 / 2x3x3 stages): 64 x 64 tiles, three per CU
     const dim3 g = conv_grid(p, gx64, ny64);
-    convnd_igemm<T, 64, 64, 2, 2, 3, 3, UT><<<g, 256, 0, st>>>(p);
-  } else if (p.Cout % 128 == 0 && (long long)gx256 * ny128 >= 448) {
+    convnd_igemm<T, 64, 64, 2, 2, 3, 3, UT, IL><<<g, 256, 0, st>>>(p);
+  } else if (p.Cout % 128 == 0 && (long long)gx256 * ny128 >= nd256_min) {
     // 256 x 128 tiles (8 waves, 144 KB ring, one per CU: 48 KB global -> LDS per
     // 4.2 MFLOP, twice the 128 x 64 tile's intensity) when the grid still fills
-    // the chip about twice over and no column tile is half empty
+    // the chip at least once (ResNet's 7x7 layers: 392 tiles, 1.2-1.35x faster
+    // than 128 x 64 ones; FAC_ND256_MIN, same-box config 5 +2 %) and no column
+    // tile is half empty
     const dim3 g = conv_grid(p, gx256, ny128);
-    convnd_igemm<T, 256, 128, 4, 2, 1, 3, UT><<<g, 512, 0, st>>>(p);
+    convnd_igemm<T, 256, 128, 4, 2, 1, 3, UT, IL><<<g, 512, 0, st>>>(p);
   } else {
     const dim3 g = conv_grid(p, gx128, ny64);
-    convnd_igemm<T, 128, 64, 2, 2, 2, 3, UT><<<g, 256, 0, st>>>(p);
+    convnd_igemm<T, 128, 64, 2, 2, 2, 3, UT, IL><<<g, 256, 0, st>>>(p);
   }
 }
 
@@ -1296,8 +1418,16 @@ static hipError_t launch_convnd(ConvP p, int cout_pad, hipStream_t st) {
     const char* e = std::getenv("FAC_CONV_UT");
     return !(e && e[0] == '0');
   }();
-  if (ut_on && p.C8 % 8 == 0) launch_convnd_t<T, true>(p, st);
-  else launch_convnd_t<T, false>(p, st);
+  static const bool il_on = [] {
+    const char* e = std::getenv("FAC_ND_IL");
+    return !(e && e[0] == '0');
+  }();
+  if (ut_on && p.C8 % 8 == 0) {
+    if (il_on) launch_convnd_t<T, true, true>(p, st);
+    else launch_convnd_t<T, true, false>(p, st);
+  } else {
+    launch_convnd_t<T, false, false>(p, st);
+  }
   return hipGetLastError();
 }
 

@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 from torch import nn
@@ -185,6 +186,7 @@ class ResVitKan(nn.Module):
     # ms at 128 / 64 / 32 — the layers are not HBM-bound, the smaller grids
     # just fill the 256 CUs worse (tools/rvk_chunks.sh)
     feature_chunk = 0
+    side_downsample = os.environ.get("FAC_RVK_SIDE", "1") != "0"
 
     def _side_stream(self, device: torch.device):
         st = getattr(self, "_side", None)
@@ -209,7 +211,7 @@ class ResVitKan(nn.Module):
             x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))    # MaxPool2d(3, 2, 1)
             tap(x)
             for c1, c2, c3, ds in self._blocks:
-                if ds is not None:
+                if ds is not None and self.side_downsample:
                     # the downsample branch (first block of each layer) runs on a
                     # side stream beside conv1 -> conv2, joined before conv3 adds it
                     main = torch.cuda.current_stream(x.device)
@@ -220,7 +222,7 @@ class ResVitKan(nn.Module):
                     h = c2(c1(x))
                     main.wait_stream(side)
                 else:
-                    res = x
+                    res = x if ds is None else ds(x, relu=False)
                     h = c2(c1(x))
                 x = c3(h, residual=res, relu2=True)                 # relu(bn3) + residual, relu
                 tap(x)
