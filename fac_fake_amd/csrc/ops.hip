@@ -1343,6 +1343,230 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero slices landed before LDS is released
 }
 
+// ---- convnd_pt: persistent implicit GEMM for the uniform-tap (cin % 64 == 0)
+// convs with a dense 16-bit output and no residual (ResNet-50's K >= 256 1x1
+// and stride-2 convs, S3D's wide layers): convnd_igemm with three changes.
+//   * Persistent: one workgroup per CU walks row tiles of ONE column block
+//     (its weights pointer and biases fixed), and the stage ring runs across
+//     tile boundaries: the next tile's first stages are already in flight
+//     while this tile's last step computes and its outputs are stored.  Per
+//     256 x 128 tile convnd_igemm spent ~7-10k cycles in its prologue and ~7k
+//     in its LDS-staged epilogue beside 2.4k per K step (s_memtime stamps,
+//     tools/ubench/nd_ubench.hip), and with one workgroup per CU nothing
+//     overlapped them.
+//   * Transposed MFMAs (rows = channels, as conv_pw): a lane ends with 4
+//     channels of one position; tile pairs compute channels 32p + 8g + 0..3 /
+//     4..7 (weight row i of tile 2p+h is channel 32p + 8(i>>2) + 4h + (i&3)),
+//     so each lane stores 16 bytes from registers: no LDS staging, which the
+//     ring fills anyway.
+//   * BN = 256 (two ring slots of 64 KB): 64 KB through the TA per 4.2M MACs,
+//     2/3 of the 256 x 128 tile's bytes per MAC — the CU's glds issue
+//     (~37 B/clk) was what bounded that tile's K step.
+// LDS images: rows of 64 k (128 B).  A (positions): piece c of row r at
+// c ^ ((r >> 1) & 7); B (weights): at c ^ fB(r), fB(r) = ((r >> 1) & 1) |
+// (((r >> 3) & 3) << 1), conflict-free for the permuted rows a fragment
+// read touches (rows 8(i>>2) + (i&3) + 4h + 32p + 64wn, i = 0..15).
+// Stage g's glds go out during step g - D (D = NS - 1), one piece after
+// each MFMA group; output stores are counted in the vmcnt waits.
+template <class T, int BN>
+__global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
+  constexpr int BM = 256, BK = 64, NW = 8;
+  constexpr int WNW = BN / 64, WMW = NW / WNW;  // waves along N (64 channels each) and M
+  constexpr int WTM = BM / WMW, RT = WTM / 16, CT = 4;
+  constexpr int NS = BN == 256 ? 2 : 3, D = NS - 1;
+  constexpr int SLOT_A = BM * BK, SLOT = (BM + BN) * BK;
+  constexpr int NA = BM / 8 / NW, NB = BN / 8 / NW, PER = NA + NB;
+  constexpr int KH = BK / 32;
+  constexpr int QPK = D == 1 ? PER : (PER + KH - 1) / KH;  // pieces issued per K half (D = 1: all in the first)
+  constexpr int NST = RT * CT / 2;                          // output stores per lane per tile
+  static_assert(QPK <= RT && NST <= 24 && D * PER + NST <= 63, "piece / store counts");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int wm = wave / WNW, wn = wave % WNW;
+  const int G = gridDim.x;
+  int b = blockIdx.x;
+  if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);  // consecutive b on one XCD
+  const int ny = p.Cout / BN, nrt = (p.M + BM - 1) / BM;
+  const int cb = b % ny, rstep = G / ny;
+  const int n0 = cb * BN;
+  int rt_first = b / ny;
+  const int ntile = rt_first < nrt ? (nrt - 1 - rt_first) / rstep + 1 : 0;
+  const int S = p.ksteps, total = ntile * S;
+
+  // glds lane geometry: instruction i of this wave covers image rows
+  // 8 (NW i + wave) + (lane >> 3), position lane & 7
+  const int pos = lane & 7, rsub = lane >> 3;
+  const int jA = pos ^ ((4 * wave + (lane >> 4)) & 7);
+  const int jB = pos ^ (((lane >> 4) & 1) | ((wave & 3) << 1));
+  const uint16_t* wsrc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) wsrc[i] = p.w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * p.Kp + jB * 8;
+  // biases of this lane's output channels (fixed: one column block per workgroup)
+  float bv[CT][4];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bv[ct][j] = p.bias ? p.bias[n0 + wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
+
+  // wait for the bias loads here, once (not beside the glds in flight later)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) asm volatile("" : "+v"(bv[ct][0]), "+v"(bv[ct][1]), "+v"(bv[ct][2]), "+v"(bv[ct][3]));
+
+  // issue cursor: row tile, step, per-A-instruction row offsets and tap bases
+  int i_rt = rt_first, i_s = 0, uc = 0, uz = 0, uy = 0, ux = 0, i_stage = 0;
+  long long roff[NA];
+  int riz[NA], riy[NA], rix[NA];
+  const long long rowstride = (long long)p.W * p.C8 * 8, planestride = rowstride * p.H;
+  auto set_rows = [&](int rt_idx) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int m = rt_idx * BM + 8 * (NW * i + wave) + rsub;
+      const int mm = m < p.M ? m : 0;
+      const int ox = mm % p.Wo, t1 = mm / p.Wo;
+      const int oy = t1 % p.Ho, t2 = t1 / p.Ho;
+      const int oz = t2 % p.Do, n = t2 / p.Do;
+      riz[i] = m < p.M ? oz * p.SD - p.PD : -(1 << 29);
+      riy[i] = oy * p.SH - p.PH;
+      rix[i] = ox * p.SW - p.PW;
+      roff[i] = (long long)n * p.D * planestride + ((long long)riz[i] * p.H + riy[i]) * rowstride +
+                (long long)rix[i] * (p.C8 * 8) + jA * 8;
+    }
+  };
+  set_rows(i_rt);
+  // piece q of the stage at the cursor (A pieces, then B); stages past the
+  // workgroup's last copy zeros into slots never read
+  auto piece = [&](int q) {
+    uint16_t* slot = smem + (i_stage % NS) * SLOT;
+    const bool real = i_stage < total;
+    if (q < NA) {
+      const long long toff = uz * planestride + uy * rowstride + (long long)ux * p.C8 * 8 + uc;
+      const bool ok = real & ((unsigned)(riz[q] + uz) < (unsigned)p.D) & ((unsigned)(riy[q] + uy) < (unsigned)p.H) &
+                      ((unsigned)(rix[q] + ux) < (unsigned)p.W);
+      glds16(ok ? p.in + (roff[q] + toff) : g_zero16, slot + (NW * q + wave) * 64 * 8);
+    } else {
+      glds16(real ? wsrc[q - NA] + (size_t)i_s * BK : g_zero16, slot + SLOT_A + (NW * (q - NA) + wave) * 64 * 8);
+    }
+  };
+  auto advance = [&] {
+    ++i_stage;
+    uc += 64;
+    if (uc == p.C8 * 8) {
+      uc = 0;
+      if (++ux == p.KW) {
+        ux = 0;
+        if (++uy == p.KH) {
+          uy = 0;
+          ++uz;
+        }
+      }
+    }
+    if (++i_s == S) {
+      i_s = uc = uz = uy = ux = 0;
+      i_rt += rstep;
+      if (i_stage < total) set_rows(i_rt);
+    }
+  };
+
+  f32x4 acc[RT][CT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = (f32x4)0.f;
+
+#pragma unroll
+  for (int st = 0; st < D; ++st) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) piece(q);
+    advance();
+  }
+  int c_rt = rt_first, c_s = 0;
+  // ends[k]: step g-1-k ended a tile (its NST output stores follow stage g-1-k+D's pieces)
+  int end1 = 0, end2 = 0;
+  for (int gs = 0; gs < total; ++gs) {
+#ifdef ND_STAMPS
+    const int s = gs;
+#endif
+    ND_STAMP(0);
+    // stage gs landed: younger are stages gs+1 .. gs+D-1 and the stores of
+    // the tile ends among steps gs-D .. gs-1
+    const int nend = end1 + (D >= 2 ? end2 : 0);
+    if (D == 1) {
+      if (nend) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+      if (nend) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((D - 1) * PER + NST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((D - 1) * PER) : "memory");
+    }
+    ND_STAMP(1);
+    const uint16_t* a = smem + (gs % NS) * SLOT;
+    const uint16_t* bw = a + SLOT_A;
+#pragma unroll
+    for (int ks = 0; ks < KH; ++ks) {
+      const int c = ks * 4 + g;
+      u16x8 fw[CT], fp[RT];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int r = wn * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
+        const int fB = ((r >> 1) & 1) | (((r >> 3) & 3) << 1);
+        fw[ct] = *(const u16x8*)(bw + r * BK + ((c ^ fB) << 3));
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int r = wm * WTM + rt * 16 + r16;
+        fp[rt] = *(const u16x8*)(a + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = T::mfma(fw[ct], fp[rt], acc[rt][ct]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (rt < QPK && ks * QPK + rt < PER) piece(ks * QPK + rt);
+      }
+    }
+    ND_STAMP(2);
+    advance();
+    end2 = end1;
+    end1 = 0;
+    if (++c_s == S) {
+      // tile done: bias, ReLU, 16-byte stores from registers
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int m = c_rt * BM + wm * WTM + rt * 16 + r16;
+        if (m < p.M) {
+          uint16_t* o = (uint16_t*)p.out + (size_t)m * p.ldo + p.c_off + n0 + wn * 64 + 8 * g;
+#pragma unroll
+          for (int pp = 0; pp < CT / 2; ++pp) {
+            u16x4 q2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              f32x4 v;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const float x = acc[rt][2 * pp + h][j] + bv[2 * pp + h][j];
+                v[j] = (p.flags & FAC_CONV_RELU) ? relu(x) : x;
+              }
+              q2[h] = T::pack4(v);
+            }
+            *(u16x8*)(o + 32 * pp) = __builtin_shufflevector(q2[0], q2[1], 0, 1, 2, 3, 4, 5, 6, 7);
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = (f32x4)0.f;
+      }
+      c_s = 0;
+      c_rt += rstep;
+      end1 = 1;
+    }
+    ND_STAMP(3);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero stages landed before LDS is released
+}
+
 // grid of gx row tiles x ny column tiles: flat (column tiles of a row tile
 // adjacent, see convnd_igemm) unless FAC_CONV_FLAT=0 or it would overflow
 static dim3 conv_grid(ConvP& p, int gx, int ny) {
@@ -1358,8 +1582,39 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
   return dim3(gx, ny);
 }
 
+template <class T>
+static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
+  static const int pt_mode = [] {
+    const char* e = std::getenv("FAC_ND_PT");  // 0 off, 128 / 256 force the tile width
+    return e ? std::atoi(e) : 1;
+  }();
+  if (!pt_mode || p.Cout % 128 || p.ksteps < 2 || !p.vec_out || p.split1 < p.Cout ||
+      (p.flags & (FAC_CONV_RESID | FAC_CONV_OUT_F32 | FAC_CONV_RELU2)))
+    return false;
+  static const int ncu = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int nrt = (p.M + 255) / 256;
+  const int bn = pt_mode == 128 || pt_mode == 256 ? pt_mode : (p.Cout % 256 == 0 ? 256 : 128);
+  if (p.Cout % bn) return false;
+  const int ny = p.Cout / bn;
+  int G = ncu / ny * ny;
+  if ((long long)nrt * ny < G) G = nrt * ny;
+  if (G <= 0) return false;
+  p.ny = 0;
+  if (bn == 256) convnd_pt<T, 256><<<G, 512, 0, st>>>(p);
+  else convnd_pt<T, 128><<<G, 512, 0, st>>>(p);
+  return true;
+}
+
 template <class T, bool UT, bool IL>
 static void launch_convnd_t(ConvP p, hipStream_t st) {
+  if constexpr (UT) {
+    if (launch_convnd_pt<T>(p, st)) return;
+  }
   const int gx64 = (p.M + 63) / 64, gx128 = (p.M + 127) / 128, gx256 = (p.M + 255) / 256;
   const int ny64 = (p.Cout + 63) / 64, ny128 = (p.Cout + 127) / 128;
   // FAC_ND_TILE forces one tile (layer A/Bs: tools/nd_layers.py): 1 = 128x64

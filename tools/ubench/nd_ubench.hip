@@ -78,9 +78,9 @@ int main(int argc, char** argv) {
   printf("%s, %d crops: %.1f us, %d K steps\n", l.name, B, ms * 1e3, ksteps);
   static unsigned long long st[8][40][8][4];
   (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(fac::nd_st), sizeof(st));
-  const int s1 = std::min(ksteps - 1, 39);
+  const int s1 = 39;  // convnd_pt: stamps run over the workgroup's steps across tiles
   for (int wg = 0; wg < 3; ++wg) {
-    printf("wg %d, mean ticks over steps 1..%d per wave: [issue] [reads+MFMA issue] [wait] [barrier->next]\n", wg, s1 - 1);
+    printf("wg %d, mean ticks over steps 1..%d per wave: [0->1] [1->2] [2->3] [3->next 0]\n", wg, s1 - 1);
     for (int w = 0; w < 8; ++w) {
       double a = 0, b = 0, c = 0, e = 0;
       int n = 0;
