@@ -1368,7 +1368,11 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
 // read touches (rows 8(i>>2) + (i&3) + 4h + 32p + 64wn, i = 0..15).
 // Stage g's glds go out during step g - D (D = NS - 1), one piece after
 // each MFMA group; output stores are counted in the vmcnt waits.
-template <class T, int BN>
+// RES (BN = 128 only): the residual's 16-byte vectors of a tile go out as
+// inline-asm loads at the start of its last K step (hipcc would wait
+// vmcnt(0) for an ordinary load beside glds in flight) and are waited for
+// by count in the epilogue (only that step's glds pieces are younger).
+template <class T, int BN, bool RES = false>
 __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
   constexpr int BM = 256, BK = 64, NW = 8;
   constexpr int WNW = BN / 64, WMW = NW / WNW;  // waves along N (64 channels each) and M
@@ -1380,6 +1384,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
   constexpr int QPK = D == 1 ? PER : (PER + KH - 1) / KH;  // pieces issued per K half (D = 1: all in the first)
   constexpr int NST = RT * CT / 2;                          // output stores per lane per tile
   static_assert(QPK <= RT && NST <= 24 && D * PER + NST <= 63, "piece / store counts");
+  static_assert(!RES || BN == 128, "residual: 128-wide tiles (register budget)");
   __shared__ __attribute__((aligned(16))) uint16_t smem[NS * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1504,6 +1509,21 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
     ND_STAMP(1);
     const uint16_t* a = smem + (gs % NS) * SLOT;
     const uint16_t* bw = a + SLOT_A;
+    // RES: the residual vectors of this tile's lanes, at its last step
+    u16x8 rv[RES ? RT : 1][RES ? CT / 2 : 1];
+    if constexpr (RES) {
+      if (c_s == S - 1) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          const int m = c_rt * BM + wm * WTM + rt * 16 + r16;
+#pragma unroll
+          for (int pp = 0; pp < CT / 2; ++pp) {
+            const uint16_t* src = m < p.M ? p.res + (size_t)m * p.ldr + p.r_off + n0 + wn * 64 + 32 * pp + 8 * g : g_zero16;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rv[rt][pp]) : "v"(src) : "memory");
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < KH; ++ks) {
       const int c = ks * 4 + g;
@@ -1533,7 +1553,16 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
     end2 = end1;
     end1 = 0;
     if (++c_s == S) {
-      // tile done: bias, ReLU, 16-byte stores from registers
+      // tile done: bias, ReLU (+ residual, ReLU), 16-byte stores from registers
+      if constexpr (RES) {
+        // the residual loads landed: younger are this step's PER glds pieces
+        static_assert(RT * CT / 2 == 8, "residual wait ties 8 vectors");
+        asm volatile("s_waitcnt vmcnt(%8)"
+                     : "+v"(rv[0][0]), "+v"(rv[0][1]), "+v"(rv[1][0]), "+v"(rv[1][1]), "+v"(rv[2][0]), "+v"(rv[2][1]),
+                       "+v"(rv[3][0]), "+v"(rv[3][1])
+                     : "n"(PER)
+                     : "memory");
+      }
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         const int m = c_rt * BM + wm * WTM + rt * 16 + r16;
@@ -1547,8 +1576,13 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
               f32x4 v;
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
-                const float x = acc[rt][2 * pp + h][j] + bv[2 * pp + h][j];
-                v[j] = (p.flags & FAC_CONV_RELU) ? relu(x) : x;
+                float x = acc[rt][2 * pp + h][j] + bv[2 * pp + h][j];
+                if (p.flags & FAC_CONV_RELU) x = relu(x);
+                if constexpr (RES) {
+                  x += T::to_f32(rv[rt][pp][4 * h + j]);
+                  if (p.flags & FAC_CONV_RELU2) x = relu(x);
+                }
+                v[j] = x;
               }
               q2[h] = T::pack4(v);
             }
@@ -1588,8 +1622,9 @@ static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
     const char* e = std::getenv("FAC_ND_PT");  // 0 off, 128 / 256 force the tile width
     return e ? std::atoi(e) : 1;
   }();
+  const bool res = p.flags & FAC_CONV_RESID;
   if (!pt_mode || p.Cout % 128 || p.ksteps < 2 || !p.vec_out || p.split1 < p.Cout ||
-      (p.flags & (FAC_CONV_RESID | FAC_CONV_OUT_F32 | FAC_CONV_RELU2)))
+      (p.flags & FAC_CONV_OUT_F32) || (!res && (p.flags & FAC_CONV_RELU2)) || (res && !p.vec_res))
     return false;
   static const int ncu = [] {
     int dev = 0, n = 256;
@@ -1598,14 +1633,15 @@ static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
     return n;
   }();
   const int nrt = (p.M + 255) / 256;
-  const int bn = pt_mode == 128 || pt_mode == 256 ? pt_mode : (p.Cout % 256 == 0 ? 256 : 128);
+  const int bn = res ? 128 : (pt_mode == 128 || pt_mode == 256 ? pt_mode : (p.Cout % 256 == 0 ? 256 : 128));
   if (p.Cout % bn) return false;
   const int ny = p.Cout / bn;
   int G = ncu / ny * ny;
   if ((long long)nrt * ny < G) G = nrt * ny;
   if (G <= 0) return false;
   p.ny = 0;
-  if (bn == 256) convnd_pt<T, 256><<<G, 512, 0, st>>>(p);
+  if (res) convnd_pt<T, 128, true><<<G, 512, 0, st>>>(p);
+  else if (bn == 256) convnd_pt<T, 256><<<G, 512, 0, st>>>(p);
   else convnd_pt<T, 128><<<G, 512, 0, st>>>(p);
   return true;
 }
@@ -1788,7 +1824,14 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     const char* e = std::getenv("FAC_PW_K256");
     return !(e && e[0] == '0');
   }();
-  if (pw_on && !split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+  static const bool pw_pt = [] {
+    // K 128 / 256 1x1s with cout % 128 == 0 go to convnd_pt (FAC_PW_PT=0: conv_pw):
+    // config 5 +1.2 % same-box (layer3's 256 -> 1024 + residual 160 -> 145 us)
+    const char* e = std::getenv("FAC_PW_PT");
+    return !(e && e[0] == '0');
+  }();
+  const bool to_pt = pw_pt && (d->cin == 128 || d->cin == 256) && d->cout % 128 == 0;
+  if (pw_on && !split && !to_pt && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
       d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->cin == 64 || d->cin == 128 || (d->cin == 256 && pw256)) &&
       k_pad == d->cin &&
       d->cout % 64 == 0 && d->ldo % 8 == 0 && d->c_off % 8 == 0 && !(d->flags & FAC_CONV_OUT_F32) &&
