@@ -115,7 +115,7 @@ __device__ unsigned long long nd_ev[8][8][4];  // per wave: entry, prologue done
 // gather is one precomputed row offset + a wave-uniform step offset per A
 // piece, validity by three unsigned compares, and no per-lane (channel piece,
 // tap) tracking or per-piece branches (the generic path's VALU work was ~8.5
-// instructions per MFMA on the ResNet-50 layers: profiles/r03_resvitkan_pmc.json).
+// instructions per MFMA on the ResNet-50 layers in a round-3 SQ_INSTS_VALU pass).
 //
 // IL (interleaved issue, UT only): the next stage's glds pieces are issued
 // one at a time between the step's MFMA groups instead of all at the step
