@@ -177,7 +177,9 @@ def layer_roofline_ms(run, dtype: str) -> dict:
     """Per-layer roofline of the fac_conv_nd / fac_pool_nd layers one eager
     `run()` launches: each layer bounded by max(algorithmic FLOPs / dense
     MFMA peak, minimum HBM bytes (input read once, output (+ residual)
-    written / read once) / HBM peak), summed.  The ResNet-50 and S3D layers
+    written / read once) / HBM peak), summed; ResNet's conv3 with its fused
+    downsample (ops.conv_dual) is one op whose bytes exclude the residual it
+    no longer writes and reads.  The ResNet-50 and S3D layers
     at these batch sizes are mostly HBM-bound (arithmetic intensity under the
     ~312 FLOP/B ridge), so the MFMA-only fraction understates them."""
     from fac_fake_amd import ops, resvitkan, s3d
@@ -196,6 +198,16 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         recs.append((flops, byts))
         return out
 
+    orig_dual = ops.conv_dual
+
+    def dual_hook(layer, h, ds, x, **kw):   # conv3 + fused downsample: one op, its own minimum bytes
+        out = orig_dual(layer, h, ds, x, **kw)
+        M = out.numel() // layer.cout
+        flops = 2.0 * M * layer.cout * (layer.g.kd * layer.g.kh * layer.g.kw * layer.cin
+                                        + ds.g.kd * ds.g.kh * ds.g.kw * ds.cin)
+        recs.append((flops, 2.0 * (h.numel() + x.numel() + out.numel())))
+        return out
+
     def pool_hook(x, *a, **kw):
         out = orig_pool(x, *a, **kw)
         if not in_sep[0]:
@@ -212,6 +224,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         return out
 
     ops.ConvLayer.__call__ = conv_hook
+    ops.conv_dual = resvitkan.conv_dual = dual_hook
     ops.pool = resvitkan.pool = s3d.pool = pool_hook
     resvitkan.max_pool_sep = s3d.max_pool_sep = sep_hook
     try:
@@ -219,6 +232,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         torch.cuda.synchronize()
     finally:
         ops.ConvLayer.__call__ = orig_call
+        ops.conv_dual = resvitkan.conv_dual = orig_dual
         ops.pool = resvitkan.pool = s3d.pool = orig_pool
         resvitkan.max_pool_sep = s3d.max_pool_sep = orig_sep
     peak = PEAK_TFLOPS[dtype] * 1e12

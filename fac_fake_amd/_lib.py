@@ -57,6 +57,7 @@ SIGNATURES = {
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     # include/fac_ops.h
     "fac_conv_nd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "fac_conv_nd_dual": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_conv_weight_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "fac_pool_nd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

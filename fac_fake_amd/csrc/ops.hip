@@ -1372,8 +1372,15 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
 // inline-asm loads at the start of its last K step (hipcc would wait
 // vmcnt(0) for an ordinary load beside glds in flight) and are waited for
 // by count in the epilogue (only that step's glds pieces are younger).
-template <class T, int BN, bool RES = false>
-__global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
+// DUAL (BN = 128, no RES): a second GEMM q over another input into the same
+// output positions and channels — ResNet's downsample branch fused into the
+// bottleneck's conv3.  A tile runs conv3's K steps, then in registers
+// acc = relu(acc + b3) + b_ds (the reference's ReLU after bn3 comes before
+// the residual add, ResVitKan.py:146-152), then the downsample's K steps
+// (its input gathered with its own geometry and stride), then relu: the
+// downsample output never goes through HBM.
+template <class T, int BN, bool RES = false, bool DUAL = false>
+__global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
   constexpr int BM = 256, BK = 64, NW = 8;
   constexpr int WNW = BN / 64, WMW = NW / WNW;  // waves along N (64 channels each) and M
   constexpr int WTM = BM / WMW, RT = WTM / 16, CT = 4;
@@ -1385,6 +1392,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
   constexpr int NST = RT * CT / 2;                          // output stores per lane per tile
   static_assert(QPK <= RT && NST <= 24 && D * PER + NST <= 63, "piece / store counts");
   static_assert(!RES || BN == 128, "residual: 128-wide tiles (register budget)");
+  static_assert(!DUAL || (BN == 128 && !RES), "dual GEMM: 128-wide tiles, no residual input");
   __shared__ __attribute__((aligned(16))) uint16_t smem[NS * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1398,7 +1406,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
   const int n0 = cb * BN;
   int rt_first = b / ny;
   const int ntile = rt_first < nrt ? (nrt - 1 - rt_first) / rstep + 1 : 0;
-  const int S = p.ksteps, total = ntile * S;
+  const int S1 = p.ksteps, S = DUAL ? S1 + q.ksteps : S1, total = ntile * S;
 
   // glds lane geometry: instruction i of this wave covers image rows
   // 8 (NW i + wave) + (lane >> 3), position lane & 7
@@ -1406,8 +1414,13 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
   const int jA = pos ^ ((4 * wave + (lane >> 4)) & 7);
   const int jB = pos ^ (((lane >> 4) & 1) | ((wave & 3) << 1));
   const uint16_t* wsrc[NB];
+  const uint16_t* wsrc2[DUAL ? NB : 1];
 #pragma unroll
   for (int i = 0; i < NB; ++i) wsrc[i] = p.w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * p.Kp + jB * 8;
+  if constexpr (DUAL) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) wsrc2[i] = q.w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * q.Kp + jB * 8;
+  }
   // biases of this lane's output channels (fixed: one column block per workgroup)
   float bv[CT][4];
 #pragma unroll
@@ -1416,17 +1429,51 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
     for (int j = 0; j < 4; ++j)
       bv[ct][j] = p.bias ? p.bias[n0 + wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
 
+  float bv2[DUAL ? CT : 1][4];
+  if constexpr (DUAL) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bv2[ct][j] = q.bias ? q.bias[n0 + wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
+  }
   // wait for the bias loads here, once (not beside the glds in flight later)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) asm volatile("" : "+v"(bv[ct][0]), "+v"(bv[ct][1]), "+v"(bv[ct][2]), "+v"(bv[ct][3]));
+  if constexpr (DUAL) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      asm volatile("" : "+v"(bv2[ct][0]), "+v"(bv2[ct][1]), "+v"(bv2[ct][2]), "+v"(bv2[ct][3]));
+  }
 
   // issue cursor: row tile, step, per-A-instruction row offsets and tap bases
   int i_rt = rt_first, i_s = 0, uc = 0, uz = 0, uy = 0, ux = 0, i_stage = 0;
   long long roff[NA];
   int riz[NA], riy[NA], rix[NA];
-  const long long rowstride = (long long)p.W * p.C8 * 8, planestride = rowstride * p.H;
+  // the gather geometry of the GEMM at the cursor (DUAL: p's, then q's)
+  const uint16_t* g_in = p.in;
+  int gD = p.D, gH = p.H, gW = p.W, gC8 = p.C8, gKH = p.KH, gKW = p.KW;
+  int gSD = p.SD, gSH = p.SH, gSW = p.SW, gPD = p.PD, gPH = p.PH, gPW = p.PW;
+  auto use_geo = [&](bool second) {
+    g_in = second ? q.in : p.in;
+    gD = second ? q.D : p.D;
+    gH = second ? q.H : p.H;
+    gW = second ? q.W : p.W;
+    gC8 = second ? q.C8 : p.C8;
+    gKH = second ? q.KH : p.KH;
+    gKW = second ? q.KW : p.KW;
+    gSD = second ? q.SD : p.SD;
+    gSH = second ? q.SH : p.SH;
+    gSW = second ? q.SW : p.SW;
+    gPD = second ? q.PD : p.PD;
+    gPH = second ? q.PH : p.PH;
+    gPW = second ? q.PW : p.PW;
+  };
+  long long rowstride = (long long)p.W * p.C8 * 8, planestride = rowstride * p.H;
   auto set_rows = [&](int rt_idx) {
+    rowstride = (long long)gW * gC8 * 8;
+    planestride = rowstride * gH;
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const int m = rt_idx * BM + 8 * (NW * i + wave) + rsub;
@@ -1434,36 +1481,40 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
       const int ox = mm % p.Wo, t1 = mm / p.Wo;
       const int oy = t1 % p.Ho, t2 = t1 / p.Ho;
       const int oz = t2 % p.Do, n = t2 / p.Do;
-      riz[i] = m < p.M ? oz * p.SD - p.PD : -(1 << 29);
-      riy[i] = oy * p.SH - p.PH;
-      rix[i] = ox * p.SW - p.PW;
-      roff[i] = (long long)n * p.D * planestride + ((long long)riz[i] * p.H + riy[i]) * rowstride +
-                (long long)rix[i] * (p.C8 * 8) + jA * 8;
+      riz[i] = m < p.M ? oz * gSD - gPD : -(1 << 29);
+      riy[i] = oy * gSH - gPH;
+      rix[i] = ox * gSW - gPW;
+      roff[i] = (long long)n * gD * planestride + ((long long)riz[i] * gH + riy[i]) * rowstride +
+                (long long)rix[i] * (gC8 * 8) + jA * 8;
     }
   };
   set_rows(i_rt);
   // piece q of the stage at the cursor (A pieces, then B); stages past the
   // workgroup's last copy zeros into slots never read
-  auto piece = [&](int q) {
+  auto piece = [&](int qq) {
     uint16_t* slot = smem + (i_stage % NS) * SLOT;
     const bool real = i_stage < total;
-    if (q < NA) {
-      const long long toff = uz * planestride + uy * rowstride + (long long)ux * p.C8 * 8 + uc;
-      const bool ok = real & ((unsigned)(riz[q] + uz) < (unsigned)p.D) & ((unsigned)(riy[q] + uy) < (unsigned)p.H) &
-                      ((unsigned)(rix[q] + ux) < (unsigned)p.W);
-      glds16(ok ? p.in + (roff[q] + toff) : g_zero16, slot + (NW * q + wave) * 64 * 8);
+    if (qq < NA) {
+      const long long toff = uz * planestride + uy * rowstride + (long long)ux * gC8 * 8 + uc;
+      const bool ok = real & ((unsigned)(riz[qq] + uz) < (unsigned)gD) & ((unsigned)(riy[qq] + uy) < (unsigned)gH) &
+                      ((unsigned)(rix[qq] + ux) < (unsigned)gW);
+      glds16(ok ? g_in + (roff[qq] + toff) : g_zero16, slot + (NW * qq + wave) * 64 * 8);
     } else {
-      glds16(real ? wsrc[q - NA] + (size_t)i_s * BK : g_zero16, slot + SLOT_A + (NW * (q - NA) + wave) * 64 * 8);
+      const uint16_t* wb = wsrc[qq - NA] + (size_t)i_s * BK;
+      if constexpr (DUAL) {
+        if (i_s >= S1) wb = wsrc2[qq - NA] + (size_t)(i_s - S1) * BK;
+      }
+      glds16(real ? wb : g_zero16, slot + SLOT_A + (NW * (qq - NA) + wave) * 64 * 8);
     }
   };
   auto advance = [&] {
     ++i_stage;
     uc += 64;
-    if (uc == p.C8 * 8) {
+    if (uc == gC8 * 8) {
       uc = 0;
-      if (++ux == p.KW) {
+      if (++ux == gKW) {
         ux = 0;
-        if (++uy == p.KH) {
+        if (++uy == gKH) {
           uy = 0;
           ++uz;
         }
@@ -1472,7 +1523,12 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
     if (++i_s == S) {
       i_s = uc = uz = uy = ux = 0;
       i_rt += rstep;
+      if constexpr (DUAL) use_geo(false);
       if (i_stage < total) set_rows(i_rt);
+    } else if (DUAL && i_s == S1) {
+      uc = uz = uy = ux = 0;
+      use_geo(true);
+      set_rows(i_rt);
     }
   };
 
@@ -1509,6 +1565,20 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
     ND_STAMP(1);
     const uint16_t* a = smem + (gs % NS) * SLOT;
     const uint16_t* bw = a + SLOT_A;
+    if constexpr (DUAL) {
+      if (c_s == S1) {  // conv3 done: relu(acc + b3) + b_ds, then the downsample's K steps accumulate on it
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              float x = acc[rt][ct][j] + bv[ct][j];
+              if (p.flags & FAC_CONV_RELU) x = relu(x);
+              acc[rt][ct][j] = x + bv2[ct][j];
+            }
+      }
+    }
     // RES: the residual vectors of this tile's lanes, at its last step
     u16x8 rv[RES ? RT : 1][RES ? CT / 2 : 1];
     if constexpr (RES) {
@@ -1576,8 +1646,14 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p) {
               f32x4 v;
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
-                float x = acc[rt][2 * pp + h][j] + bv[2 * pp + h][j];
-                if (p.flags & FAC_CONV_RELU) x = relu(x);
+                float x;
+                if constexpr (DUAL) {
+                  x = acc[rt][2 * pp + h][j];
+                  if (p.flags & FAC_CONV_RELU2) x = relu(x);
+                } else {
+                  x = acc[rt][2 * pp + h][j] + bv[2 * pp + h][j];
+                  if (p.flags & FAC_CONV_RELU) x = relu(x);
+                }
                 if constexpr (RES) {
                   x += T::to_f32(rv[rt][pp][4 * h + j]);
                   if (p.flags & FAC_CONV_RELU2) x = relu(x);
@@ -1640,9 +1716,9 @@ static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
   if ((long long)nrt * ny < G) G = nrt * ny;
   if (G <= 0) return false;
   p.ny = 0;
-  if (res) convnd_pt<T, 128, true><<<G, 512, 0, st>>>(p);
-  else if (bn == 256) convnd_pt<T, 256><<<G, 512, 0, st>>>(p);
-  else convnd_pt<T, 128><<<G, 512, 0, st>>>(p);
+  if (res) convnd_pt<T, 128, true><<<G, 512, 0, st>>>(p, p);
+  else if (bn == 256) convnd_pt<T, 256><<<G, 512, 0, st>>>(p, p);
+  else convnd_pt<T, 128><<<G, 512, 0, st>>>(p, p);
   return true;
 }
 
@@ -1960,6 +2036,77 @@ int fac_conv_nd_split(const fac_conv_desc* d, void* out1, int ldo1, int split1, 
       d->ldo < d->c_off + split1)
     return FAC_ERR_ARG;
   return conv_nd_impl(d, out1, ldo1, split1, out2, ldo2, split2, stream);
+}
+
+// the ConvP of a uniform-tap conv for convnd_pt (fac_conv_nd_dual); false if
+// the descriptor is malformed or not uniform-tap (cin % 64)
+static bool dual_convp(const fac_conv_desc* d, fac::ConvP& p, bool need_out) {
+  if (!d || !d->in || !d->weight || (need_out && !d->out)) return false;
+  if (d->cin <= 0 || d->cin % 64 || d->cout <= 0 || d->n <= 0 || d->d <= 0 || d->h <= 0 || d->w <= 0) return false;
+  if (d->kd <= 0 || d->kh <= 0 || d->kw <= 0 || d->sd <= 0 || d->sh <= 0 || d->sw <= 0) return false;
+  if (d->pd < 0 || d->ph < 0 || d->pw < 0) return false;
+  if (d->od != (d->d + 2 * d->pd - d->kd) / d->sd + 1 || d->oh != (d->h + 2 * d->ph - d->kh) / d->sh + 1 ||
+      d->ow != (d->w + 2 * d->pw - d->kw) / d->sw + 1)
+    return false;
+  int cout_pad, k_pad;
+  fac_conv_weight_layout(d->cout, d->cin, d->kd, d->kh, d->kw, &cout_pad, &k_pad);
+  if (d->k_pad != k_pad) return false;
+  const long long M = (long long)d->n * d->od * d->oh * d->ow;
+  if (M >= (1LL << 31) || (long long)d->n * d->d * d->h * d->w * d->cin >= (1LL << 40)) return false;
+  p = fac::ConvP{};
+  p.in = (const uint16_t*)d->in;
+  p.w = (const uint16_t*)d->weight;
+  p.bias = d->bias;
+  p.out = d->out;
+  p.D = d->d;
+  p.H = d->h;
+  p.W = d->w;
+  p.C8 = d->cin / 8;
+  p.Do = d->od;
+  p.Ho = d->oh;
+  p.Wo = d->ow;
+  p.Cout = d->cout;
+  p.KD = d->kd;
+  p.KH = d->kh;
+  p.KW = d->kw;
+  p.SD = d->sd;
+  p.SH = d->sh;
+  p.SW = d->sw;
+  p.PD = d->pd;
+  p.PH = d->ph;
+  p.PW = d->pw;
+  p.Kp = k_pad;
+  p.ksteps = k_pad / 64;
+  p.ktot8 = d->kd * d->kh * d->kw * (d->cin / 8);
+  p.ldo = d->ldo;
+  p.c_off = d->c_off;
+  p.flags = d->flags;
+  p.vec_out = (d->ldo % 8 == 0 && d->c_off % 8 == 0) ? 1 : 0;
+  p.M = (int)M;
+  p.split1 = p.split2 = INT_MAX;
+  return true;
+}
+
+int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stream) {
+  using namespace fac;
+  if (!d || !ds || d->dtype != ds->dtype || (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16)) return FAC_ERR_ARG;
+  if ((d->flags & (FAC_CONV_RESID | FAC_CONV_OUT_F32)) || ds->flags != 0) return FAC_ERR_ARG;
+  ConvP p, q;
+  if (!dual_convp(d, p, true) || !dual_convp(ds, q, false)) return FAC_ERR_SHAPE;
+  if (d->n != ds->n || d->od != ds->od || d->oh != ds->oh || d->ow != ds->ow || d->cout != ds->cout ||
+      d->cout % 128 || !p.vec_out || d->ldo < d->c_off + d->cout)
+    return FAC_ERR_SHAPE;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  const int nrt = (p.M + 255) / 256, ny = p.Cout / 128;
+  int G = ncu / ny * ny;
+  if ((long long)nrt * ny < G) G = nrt * ny;
+  if (G <= 0) return FAC_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == FAC_DTYPE_BF16) convnd_pt<BF16, 128, false, true><<<G, 512, 0, st>>>(p, q);
+  else convnd_pt<F16, 128, false, true><<<G, 512, 0, st>>>(p, q);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 
 int fac_pool_nd(const fac_pool_desc* d, void* stream) {

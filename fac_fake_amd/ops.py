@@ -221,6 +221,49 @@ class ConvLayer:
         return out
 
 
+def _desc(layer: ConvLayer, x: torch.Tensor, out: torch.Tensor | None, flags: int) -> "ConvDesc":
+    n, d, h, w, c = x.shape
+    if c != layer.cin_p or x.dtype != TORCH16[layer.dtype] or not x.is_contiguous():
+        raise ValueError(f"conv input must be contiguous {layer.dtype} [N,D,H,W,{layer.cin_p}], got "
+                         f"{x.dtype} {tuple(x.shape)}")
+    od, oh, ow = layer.out_dims(d, h, w)
+    g = layer.g
+    dsc = ConvDesc()
+    dsc.dtype = _lib.DTYPES[layer.dtype]
+    dsc.inp = x.data_ptr()
+    dsc.n, dsc.d, dsc.h, dsc.w, dsc.cin = n, d, h, w, c
+    dsc.weight, dsc.bias = layer.w.data_ptr(), layer.b.data_ptr()
+    dsc.cout, dsc.k_pad = layer.cout, layer.k_pad
+    dsc.kd, dsc.kh, dsc.kw, dsc.sd, dsc.sh, dsc.sw = g.kd, g.kh, g.kw, g.sd, g.sh, g.sw
+    dsc.pd, dsc.ph, dsc.pw = g.pd, g.ph, g.pw
+    dsc.od, dsc.oh, dsc.ow = od, oh, ow
+    if out is not None:
+        dsc.out, dsc.ldo, dsc.c_off = out.data_ptr(), out.shape[4], 0
+    dsc.flags = flags
+    return dsc
+
+
+def conv_dual(layer: ConvLayer, h: torch.Tensor, ds: ConvLayer, x: torch.Tensor,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """relu(relu(layer(h)) + ds(x)) in one fac_conv_nd_dual launch: a ResNet
+    bottleneck's conv3 + bn3 + ReLU with its downsample branch (conv + bn,
+    ResVitKan.py:146-152) added before the final ReLU, without the
+    downsample output going through memory.  Same result as
+    ``layer(h, residual=ds(x, relu=False), relu2=True)`` up to fp32 rounding
+    (the downsample's sum is not rounded to 16 bits first)."""
+    n, d, hh, w, _ = h.shape
+    od, oh, ow = layer.out_dims(d, hh, w)
+    if tuple(ds.out_dims(*x.shape[1:4])) != (od, oh, ow) or x.shape[0] != n or ds.cout != layer.cout:
+        raise ValueError("conv_dual: the two convs must produce the same output positions and channels")
+    if out is None:
+        out = torch.empty(n, od, oh, ow, layer.cout, device=h.device, dtype=h.dtype)
+    d1 = _desc(layer, h, out, RELU | RELU2)
+    d2 = _desc(ds, x, None, 0)
+    _lib.check(_lib.load().fac_conv_nd_dual(ctypes.byref(d1), ctypes.byref(d2), _stream(h)), None,
+               "fac_conv_nd_dual")
+    return out
+
+
 def conv_split(layer: ConvLayer, x: torch.Tensor, splits, out0: torch.Tensor, c_off0: int, out1: torch.Tensor,
                out2: torch.Tensor, relu: bool = True) -> None:
     """One fac_conv_nd_split launch of `layer` (a conv over concatenated

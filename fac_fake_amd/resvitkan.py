@@ -35,7 +35,8 @@ from torch import nn
 
 from . import _lib
 from .cvit import MAX_SLOTS, _Node, reference_mask_poisons
-from .ops import TORCH16, ConvLayer, KANLinearLayer, fold_bn, max_pool_sep, pack_input_s2d, pool, s2d_weight, sigmoid
+from .ops import (TORCH16, ConvLayer, KANLinearLayer, conv_dual, fold_bn, max_pool_sep, pack_input_s2d, pool, s2d_weight,
+                  sigmoid)
 from .weights import kan_grid, resnet50_blocks, resvitkan_param_specs
 
 SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
@@ -187,6 +188,7 @@ class ResVitKan(nn.Module):
     # just fill the 256 CUs worse (tools/rvk_chunks.sh)
     feature_chunk = 0
     side_downsample = os.environ.get("FAC_RVK_SIDE", "1") != "0"
+    fuse_downsample = os.environ.get("FAC_RVK_DUAL", "1") != "0"
 
     def _side_stream(self, device: torch.device):
         st = getattr(self, "_side", None)
@@ -211,6 +213,12 @@ class ResVitKan(nn.Module):
             x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))    # MaxPool2d(3, 2, 1)
             tap(x)
             for c1, c2, c3, ds in self._blocks:
+                if ds is not None and self.fuse_downsample:
+                    # conv3 + bn3 + ReLU and the downsample conv + bn in one launch
+                    # (fac_conv_nd_dual): the residual never goes through memory
+                    x = conv_dual(c3, c2(c1(x)), ds, x)
+                    tap(x)
+                    continue
                 if ds is not None and self.side_downsample:
                     # the downsample branch (first block of each layer) runs on a
                     # side stream beside conv1 -> conv2, joined before conv3 adds it

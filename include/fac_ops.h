@@ -84,6 +84,16 @@ int fac_conv_nd(const fac_conv_desc* desc, void* stream);
 int fac_conv_nd_split(const fac_conv_desc* desc, void* out1, int ldo1, int split1, void* out2, int ldo2, int split2,
                       void* stream);
 
+/* relu(conv(desc) + bias, if desc->flags has FAC_CONV_RELU) + conv(ds) +
+ * ds bias, then ReLU if desc->flags has FAC_CONV_RELU2: a ResNet bottleneck's
+ * conv3 + bn3 (+ReLU, ResVitKan.py:146-152) with its downsample branch
+ * (conv + bn, ResVitKan.py:150) added in the same launch, so the downsample
+ * output never goes through memory.  Both convs: cin % 64 == 0, the same
+ * output positions [n, od, oh, ow] and cout (% 128 == 0); ds->out is ignored
+ * and ds->flags must be 0; no FAC_CONV_RESID / FAC_CONV_OUT_F32 on desc.
+ * Replaces fac_conv_nd(ds) + fac_conv_nd(desc with residual = its output). */
+int fac_conv_nd_dual(const fac_conv_desc* desc, const fac_conv_desc* ds, void* stream);
+
 /* Weight packing geometry for fac_conv_nd: *cout_pad = cout rounded up to
  * 128, *k_pad = taps*cin rounded up to 64. */
 int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad);

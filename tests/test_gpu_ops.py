@@ -121,6 +121,40 @@ def test_conv_pw_residual_into_slot(cin, cout, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", [
+    # (n, h, cin3, hx, cin_ds, stride_ds, cout): ResNet-50 bottleneck conv3 + downsample
+    (2, 56, 64, 56, 64, 1, 256),      # layer1 (two K steps: one per GEMM)
+    (2, 28, 128, 56, 256, 2, 512),    # layer2: strided downsample gather
+    (2, 7, 512, 14, 1024, 2, 2048),   # layer4
+    (3, 13, 128, 26, 256, 2, 128),    # ragged last row tile, one column block
+])
+def test_conv_dual_vs_torch_fp32(case, dt):
+    """fac_conv_nd_dual (convnd_pt DUAL): relu(relu(conv3(h) + b3) + ds(x) +
+    b_ds) in one launch vs PyTorch fp32 of the same 16-bit operands, within one
+    16-bit ulp (the downsample sum stays fp32 until the final rounding)."""
+    from fac_fake_amd.ops import ConvLayer, conv_dual
+    n, hh, c3, hx, cds, sds, cout = case
+    g = torch.Generator().manual_seed(7 + cout + hh)
+    h = torch.randn(n, c3, 1, hh, hh, generator=g).to(T16[dt]).float()
+    x = torch.randn(n, cds, 1, hx, hx, generator=g).to(T16[dt]).float()
+    w3 = torch.randn(cout, c3, 1, 1, 1, generator=g) / np.sqrt(c3)
+    wd = torch.randn(cout, cds, 1, 1, 1, generator=g) / np.sqrt(cds)
+    b3 = torch.randn(cout, generator=g) * 0.1
+    bd = torch.randn(cout, generator=g) * 0.1
+    l3 = ConvLayer(w3, b3, 1, 0, dtype=dt, device=DEV)
+    ld = ConvLayer(wd, bd, (1, sds, sds), 0, dtype=dt, device=DEV)
+    hg = h.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    out = conv_dual(l3, hg, ld, xg)
+    torch.cuda.synchronize()
+    a = F.relu(F.conv3d(h, w3.to(T16[dt]).float(), b3))
+    r = F.conv3d(x, wd.to(T16[dt]).float(), bd, stride=(1, sds, sds))
+    ref = F.relu(a + r).permute(0, 2, 3, 4, 1).to(T16[dt])
+    u = _ulps(out.cpu(), ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
 def test_conv_nd_residual_concat_and_f32(dt):
     """Bottleneck epilogue relu(relu(conv + b) + res) into a channel slot of a
     wider buffer; and fp32 output of a 1-channel conv (S3D's final layer)."""
