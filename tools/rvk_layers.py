@@ -63,6 +63,23 @@ def main():
                     byts, e0, e1))
         return out
 
+    from fac_fake_amd import resvitkan as rvk_mod
+    orig_dual = ops.conv_dual
+
+    def timed_dual(layer, h, ds, x, **kw):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = orig_dual(layer, h, ds, x, **kw)
+        e1.record()
+        M = out.numel() // layer.cout
+        K = layer.cin + ds.g.kh * ds.g.kw * ds.cin
+        flops = 2.0 * M * layer.cout * K
+        byts = 2.0 * (h.numel() + x.numel() + out.numel())
+        rec.append((f"dual {layer.cin}+{ds.cin}/{ds.g.sh}->{layer.cout} @{h.shape[2]}", M, layer.cout, K, flops, byts,
+                    e0, e1))
+        return out
+
+    ops.conv_dual = rvk_mod.conv_dual = timed_dual
     ops.ConvLayer.__call__ = timed
     acc = defaultdict(list)
     meta = {}
