@@ -240,13 +240,15 @@ class CViT(nn.Module):
         logits, _ = self._run(x, x.shape[0], pos_index, u8=False, want_probs=False)
         return logits.fill_(float("nan")) if poison else logits
 
-    def forward_u8_pipelined(self, crops: torch.Tensor, pos_index, chunk: int = 256) -> torch.Tensor:
+    def forward_u8_pipelined(self, crops: torch.Tensor, pos_index, chunk: int = 256,
+                             equal: bool = True) -> torch.Tensor:
         """forward_u8 over more crops than one batch: the crops go in
-        ceil(n/chunk) equal chunks through fac_forward_nhwc_u8_pipelined, so
-        chunk k's encoder + head (on the context's tail stream) overlaps
-        chunk k+1's conv stack; then the current stream waits for every chunk.
-        Logits are bit-identical to one forward_u8 call (a crop's logits do
-        not depend on its batch)."""
+        ceil(n/chunk) chunks (equal ones, or with ``equal=False`` full chunks
+        of ``chunk`` and the remainder last) through
+        fac_forward_nhwc_u8_pipelined, so chunk k's encoder + head (on the
+        context's tail stream) overlaps chunk k+1's conv stack; then the
+        current stream waits for every chunk.  Logits are bit-identical to one
+        forward_u8 call (a crop's logits do not depend on its batch)."""
         if crops.dtype != torch.uint8 or crops.dim() != 4 or tuple(crops.shape[1:]) != (224, 224, 3):
             raise ValueError(f"expected uint8 crops [B,224,224,3], got {crops.dtype} {tuple(crops.shape)}")
         if not crops.is_cuda:
@@ -259,7 +261,7 @@ class CViT(nn.Module):
         if n == 0:
             return logits
         k = -(-n // max(1, int(chunk)))
-        step = -(-n // k)
+        step = -(-n // k) if equal else max(1, int(chunk))
         stream = torch.cuda.current_stream(x.device).cuda_stream
         for lo in range(0, n, step):
             hi = min(n, lo + step)

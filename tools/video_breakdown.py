@@ -45,6 +45,9 @@ def main():
     print("forward_u8 B=300 dev slots   %.3f ms" % timed(lambda: m.forward_u8(crops, pos_index=slots_d)))
     for ch in (160, 100, 64):
         print("pipelined chunk %3d          %.3f ms" % (ch, timed(lambda: m.forward_u8_pipelined(crops, slots_d, chunk=ch))))
+    for ch in (256, 224, 192):
+        print("pipelined %3d + rest         %.3f ms" % (ch, timed(lambda: m.forward_u8_pipelined(crops, slots_d, chunk=ch,
+                                                                                                equal=False))))
     print("forward_u8 B=256             %.3f ms" % timed(lambda: m.forward_u8(crops[:256], pos_index=slots_d[:256])))
     print("device score + item          %.3f ms" % timed(lambda: video.device_video_score(lg)))
     print("predict_video dense          %.3f ms" % timed(lambda: video.predict_video(m, frames, boxes, mode="dense")))
