@@ -1392,8 +1392,13 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
   constexpr int NST = RT * CT / 2;                          // output stores per lane per tile
   static_assert(QPK <= RT && NST <= 24 && D * PER + NST <= 63, "piece / store counts");
   static_assert(!RES || BN == 128, "residual: 128-wide tiles (register budget)");
-  static_assert(!DUAL || (BN == 128 && !RES), "dual GEMM: 128-wide tiles, no residual input");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[NS * SLOT];
+  static_assert(!DUAL || (BN == 128 && !RES), "dual GEMM: 128-wide tiles (register budget), no residual input");
+  // the stage ring, then the workgroup's column-block biases (fp32, BN of p's
+  // and with DUAL BN of q's): read by the epilogue / the DUAL transition
+  // instead of held in 16-32 VGPRs
+  constexpr int NBIAS = DUAL ? 2 * BN : BN;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NS * SLOT + 2 * NBIAS];
+  float* const sbias = (float*)(smem + NS * SLOT);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
@@ -1413,39 +1418,26 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
   const int pos = lane & 7, rsub = lane >> 3;
   const int jA = pos ^ ((4 * wave + (lane >> 4)) & 7);
   const int jB = pos ^ (((lane >> 4) & 1) | ((wave & 3) << 1));
+  // B (weight) glds sources of the GEMM at the issue cursor (DUAL: re-pointed
+  // at q's weights for the downsample's steps, which start at step S1)
   const uint16_t* wsrc[NB];
-  const uint16_t* wsrc2[DUAL ? NB : 1];
+  auto set_wsrc = [&](const uint16_t* w, int kp) {
 #pragma unroll
-  for (int i = 0; i < NB; ++i) wsrc[i] = p.w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * p.Kp + jB * 8;
-  if constexpr (DUAL) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) wsrc2[i] = q.w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * q.Kp + jB * 8;
+    for (int i = 0; i < NB; ++i) wsrc[i] = w + (size_t)(n0 + 8 * (NW * i + wave) + rsub) * kp + jB * 8;
+  };
+  set_wsrc(p.w, p.Kp);
+  int w_s0 = 0;  // first step of the GEMM wsrc points at
+  // biases of the workgroup's column block into LDS, before any glds is in flight
+  for (int c = tid; c < NBIAS; c += 512) {
+    const float* bsrc = c < BN ? p.bias : q.bias;
+    const int cc = c < BN ? c : c - BN;
+    sbias[c] = bsrc ? bsrc[n0 + cc] : 0.f;
   }
-  // biases of this lane's output channels (fixed: one column block per workgroup)
-  float bv[CT][4];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      bv[ct][j] = p.bias ? p.bias[n0 + wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
-
-  float bv2[DUAL ? CT : 1][4];
-  if constexpr (DUAL) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bv2[ct][j] = q.bias ? q.bias[n0 + wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
-  }
-  // wait for the bias loads here, once (not beside the glds in flight later)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) asm volatile("" : "+v"(bv[ct][0]), "+v"(bv[ct][1]), "+v"(bv[ct][2]), "+v"(bv[ct][3]));
-  if constexpr (DUAL) {
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-      asm volatile("" : "+v"(bv2[ct][0]), "+v"(bv2[ct][1]), "+v"(bv2[ct][2]), "+v"(bv2[ct][3]));
-  }
+  __syncthreads();
+  // this lane's 4 channels of channel tile ct (second = q's biases)
+  auto bias4 = [&](int ct, bool second) {
+    return *(const f32x4*)(sbias + (second ? BN : 0) + wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1));
+  };
 
   // issue cursor: row tile, step, per-A-instruction row offsets and tap bases
   int i_rt = rt_first, i_s = 0, uc = 0, uz = 0, uy = 0, ux = 0, i_stage = 0;
@@ -1500,11 +1492,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
                       ((unsigned)(rix[qq] + ux) < (unsigned)gW);
       glds16(ok ? g_in + (roff[qq] + toff) : g_zero16, slot + (NW * qq + wave) * 64 * 8);
     } else {
-      const uint16_t* wb = wsrc[qq - NA] + (size_t)i_s * BK;
-      if constexpr (DUAL) {
-        if (i_s >= S1) wb = wsrc2[qq - NA] + (size_t)(i_s - S1) * BK;
-      }
-      glds16(real ? wb : g_zero16, slot + SLOT_A + (NW * (qq - NA) + wave) * 64 * 8);
+      glds16(real ? wsrc[qq - NA] + (size_t)(i_s - w_s0) * BK : g_zero16, slot + SLOT_A + (NW * (qq - NA) + wave) * 64 * 8);
     }
   };
   auto advance = [&] {
@@ -1523,11 +1511,17 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
     if (++i_s == S) {
       i_s = uc = uz = uy = ux = 0;
       i_rt += rstep;
-      if constexpr (DUAL) use_geo(false);
+      if constexpr (DUAL) {
+        use_geo(false);
+        set_wsrc(p.w, p.Kp);
+        w_s0 = 0;
+      }
       if (i_stage < total) set_rows(i_rt);
     } else if (DUAL && i_s == S1) {
       uc = uz = uy = ux = 0;
       use_geo(true);
+      set_wsrc(q.w, q.Kp);
+      w_s0 = S1;
       set_rows(i_rt);
     }
   };
@@ -1568,15 +1562,17 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
     if constexpr (DUAL) {
       if (c_s == S1) {  // conv3 done: relu(acc + b3) + b_ds, then the downsample's K steps accumulate on it
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
+        for (int ct = 0; ct < CT; ++ct) {
+          const f32x4 b1 = bias4(ct, false), b2 = bias4(ct, true);
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct)
+          for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              float x = acc[rt][ct][j] + bv[ct][j];
+              float x = acc[rt][ct][j] + b1[j];
               if (p.flags & FAC_CONV_RELU) x = relu(x);
-              acc[rt][ct][j] = x + bv2[ct][j];
+              acc[rt][ct][j] = x + b2[j];
             }
+        }
       }
     }
     // RES: the residual vectors of this tile's lanes, at its last step
@@ -1644,6 +1640,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               f32x4 v;
+              const f32x4 b1 = DUAL ? (f32x4)0.f : bias4(2 * pp + h, false);
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
                 float x;
@@ -1651,7 +1648,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
                   x = acc[rt][2 * pp + h][j];
                   if (p.flags & FAC_CONV_RELU2) x = relu(x);
                 } else {
-                  x = acc[rt][2 * pp + h][j] + bv[2 * pp + h][j];
+                  x = acc[rt][2 * pp + h][j] + b1[j];
                   if (p.flags & FAC_CONV_RELU) x = relu(x);
                 }
                 if constexpr (RES) {
@@ -2099,6 +2096,8 @@ int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stre
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
     ncu = 256;
+  // 128-wide tiles: the 256-wide DUAL variant needs 256+ VGPRs and spills
+  // (scratch traffic would also break the hand-counted vmcnt waits)
   const int nrt = (p.M + 255) / 256, ny = p.Cout / 128;
   int G = ncu / ny * ny;
   if ((long long)nrt * ny < G) G = nrt * ny;
