@@ -15,6 +15,7 @@
 // 2x2 pooling window), so in the 16x16x32 MFMA C layout (row = 4*(lane>>4) +
 // reg) each lane holds a whole window of one channel: the 2x2 max-pool is
 // three fmaxf in registers.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -79,8 +80,15 @@ __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, 
 // 1: it is loaded between chunks, exposed, which halves the halo LDS so that
 // OCC = 3 workgroups share a CU and hide each other's exposed loads — the
 // 112^2 layers, whose 1-2 chunks leave little to pipeline within a box).
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true>
-__global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
+//
+// NBOX = 2: an 8-wave workgroup computes two boxes (waves 4k..4k+3 box k, each
+// exactly as a 4-wave workgroup would, with its own halo buffers) that share
+// the per-tap weight slices: half the weight glds per MFMA (a 1 KB wave load
+// costs ~46 SIMD cycles beside MFMAs, tools/ubench/issue_ubench.hip), at the
+// price of one barrier across both boxes.
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
+          int NBOX = 1>
+__global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
@@ -117,15 +125,18 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   constexpr int WSL = BN * CK;              // elements per tap slice
   constexpr int OPIX = POOL ? NPIX / 4 : NPIX;
   constexpr int OPS = BN + 8;
-  constexpr int OPER = HB * HALO + 3 * WSL;          // halo buffer(s) + 3-slot weight ring
-  constexpr int OSTG = (POOL ? RT * 4 : RT * 16) * OPS;  // padded: epilogue writes unguarded
+  constexpr int OPER = NBOX * HB * HALO + 3 * WSL;   // halo buffer(s) per box + 3-slot weight ring
+  constexpr int OSTGB = (POOL ? RT * 4 : RT * 16) * OPS;  // per box, padded: epilogue writes unguarded
+  constexpr int OSTG = NBOX * OSTGB;
   constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(TH % 2 == 0 && TW % 2 == 0, "window-major order needs even boxes");
   static_assert(CTW * 16 * WN == BN, "BN split");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // box-local thread / wave (everything but the shared weight ring), box index
+  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+  const int wave_g = threadIdx.x >> 6, box = NBOX > 1 ? (int)(threadIdx.x >> 8) : 0;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
   // XCD-aware box order: workgroups are dealt round-robin to the 8 XCDs
@@ -135,6 +146,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // 1.27x halo overhead with the plain order).
   int bx = blockIdx.x;
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  bx = bx * NBOX + box;
   const int b = bx / tiles_per_img;
   const int tile = bx - b * tiles_per_img;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
@@ -187,13 +199,16 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // slice in memory IS its LDS image, so wave w copies pieces
   // [256i + 64w, +64) straight into ring slot `slot`.
   constexpr int WPIECES = BN * CK / 8;
-  constexpr int WPW = (WPIECES + 255) / 256;  // glds instructions per wave per slice
-  uint16_t* const wring = smem + HB * HALO;
+  constexpr int WPT = 256 * NBOX;              // threads loading a slice
+  constexpr int WPW = (WPIECES + WPT - 1) / WPT;  // glds instructions per wave per slice
+  static_assert(NBOX == 1 || WPIECES % WPT == 0, "every wave issues the same slice pieces");
+  uint16_t* const wring = smem + NBOX * HB * HALO;
+  uint16_t* const hbase = smem + box * HB * HALO;  // this box's halo buffer(s)
   auto issue_w = [&](int slot, const uint16_t* src) {
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
-      const int pb = i * 256 + wave * 64;
-      if (WPIECES % 256 == 0 || pb < WPIECES) glds16(src + (size_t)(pb + lane) * 8, wring + slot * WSL + pb * 8);
+      const int pb = i * WPT + wave_g * 64;
+      if (WPIECES % WPT == 0 || pb < WPIECES) glds16(src + (size_t)(pb + lane) * 8, wring + slot * WSL + pb * 8);
     }
   };
 
@@ -230,7 +245,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   issue_w(0, wsrc);
   issue_w(1, wsrc + WSL);
   if constexpr (PB) issue_w(2, nsteps > 2 ? wsrc + 2 * WSL : wsrc);
-  issue_halo(smem, 0);
+  issue_halo(hbase, 0);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   // PB: the B fragments of tap t+1 are read during tap t as well (slice s+1
   // is retired one barrier earlier, slice s+3 is issued at step s into the
@@ -248,21 +263,21 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // MFMA skeleton of this tile goes from 67% to 80% of the MFMA floor).
   u16x8 fa[RTW];
 #pragma unroll
-  for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(smem + abase[rt]);
+  for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(hbase + abase[rt]);
   // PB: slot 0 is re-filled at step 0, after every wave has read slice 0
   if constexpr (PB) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   for (int c = 0; c < nchunks; ++c) {
     if constexpr (HB == 1) {
       if (c > 0) {  // every wave is past the previous chunk's last barrier
-        issue_halo(smem, c);
+        issue_halo(hbase, c);
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
-        for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(smem + abase[rt]);
+        for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(hbase + abase[rt]);
       }
     }
-    const uint16_t* hb = smem + (HB == 2 ? (c & 1) * HALO : 0);
-    const uint16_t* hbn = smem + (HB == 2 ? ((c + 1) & 1) * HALO : 0);
+    const uint16_t* hb = hbase + (HB == 2 ? (c & 1) * HALO : 0);
+    const uint16_t* hbn = hbase + (HB == 2 ? ((c + 1) & 1) * HALO : 0);
     const bool next_h = c + 1 < nchunks;
     const uint16_t* wnext = wsrc + (size_t)(c * 9 + 2) * WSL;
     auto step = [&](auto tc) {
@@ -275,7 +290,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
         issue_w(t % 3, (c * 9 + t + 3 < nsteps) ? wnext + (t + 1) * WSL : wsrc);
       else
         issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
-      if (HB == 2 && t == 0) issue_halo(smem + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
+      if (HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
       u16x8 bfr[CTW], bnx[CTW];
       if constexpr (PB) {
 #pragma unroll
@@ -348,7 +363,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   __syncthreads();
 
   // Epilogue: folded-BN bias + ReLU (+ 2x2 max) -> 16-bit -> LDS -> global.
-  uint16_t* ostg = smem;
+  uint16_t* ostg = smem + box * OSTGB;
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct) {
     const int nl = (wn * CTW + ct) * 16 + (lane & 15);
@@ -510,22 +525,34 @@ int conv_block_n(int H, int cout) {
 
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
 // spill with it; no model pools after such a layer)
-template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true>
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true,
+          int NBOX = 1>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
-  dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
+  const int nbox = B * (H / TH) * (H / TW);
+  if (nbox % NBOX) return hipErrorInvalidValue;
+  dim3 grid(nbox / NBOX, Cout / BN);
   if constexpr (POOLED) {
     if (pool) {
-      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
-          <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, NBOX>
+          <<<grid, 256 * NBOX, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
-      <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, NBOX>
+      <<<grid, 256 * NBOX, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
+}
+
+// FAC_CONV_NBOX=2: the 56 / 28 tiles as 8-wave two-box workgroups
+static int conv_nbox() {
+  static const int n = [] {
+    const char* e = std::getenv("FAC_CONV_NBOX");
+    return e && e[0] == '2' ? 2 : 1;
+  }();
+  return n;
 }
 
 template <class T>
@@ -538,11 +565,26 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
     // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
     case 112064: launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 56128: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 56128:
+      if (conv_nbox() == 2 && (B * 14) % 2 == 0) {
+        if (launch_box<T, 8, 28, 128, 2, 2, 2, 1, true, true, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
+          return hipErrorInvalidValue;
+      } else {
+        launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      }
+      break;
     case 56064: launch_box<T, 8, 28, 64, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 28256: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28256:
+      if (conv_nbox() == 2 && (B * 7) % 2 == 0) {
+        if (launch_box<T, 4, 28, 256, 1, 4, 2, 1, true, true, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
+          return hipErrorInvalidValue;
+      } else {
+        launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      }
+      break;
     case 28192: launch_box<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28128: launch_box<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    // (a two-box 14x14 workgroup needs 256+ VGPRs and spills: not built)
     case 14128: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 14192:
       if (launch_box<T, 14, 14, 192, 1, 4, 2, 2, false, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
