@@ -47,6 +47,39 @@ def test_version_and_null_safety(built_lib):
     lib.fac_destroy(None)
 
 
+def test_conv_nd_dual_argument_checks(built_lib):
+    """fac_conv_nd_dual rejects bad descriptors before touching the GPU: null
+    pointers / mixed dtypes / a residual flag (FAC_ERR_ARG), a non-uniform-tap
+    cin or mismatched output positions (FAC_ERR_SHAPE)."""
+    import ctypes as C
+    from fac_fake_amd import _lib
+    from fac_fake_amd.ops import ConvDesc
+    lib = _lib.load()
+    assert lib.fac_conv_nd_dual(None, None, None) == -1
+
+    def desc(cin, h, s, cout=256):
+        d = ConvDesc()
+        d.dtype, d.inp, d.weight, d.out = 0, 16, 16, 16
+        d.n, d.d, d.h, d.w, d.cin, d.cout = 2, 1, h, h, cin, cout
+        d.kd = d.kh = d.kw = 1
+        d.sd, d.sh, d.sw = 1, s, s
+        d.od, d.oh, d.ow = 1, (h - 1) // s + 1, (h - 1) // s + 1
+        d.k_pad = (cin + 63) // 64 * 64
+        d.ldo = cout
+        return d
+
+    a, b = desc(128, 28, 1), desc(256, 56, 2)
+    bad = desc(128, 28, 1)
+    bad.dtype = 1
+    assert lib.fac_conv_nd_dual(C.byref(bad), C.byref(b), None) == -1          # mixed dtypes
+    r = desc(128, 28, 1)
+    r.flags = 2                                                                   # FAC_CONV_RESID
+    assert lib.fac_conv_nd_dual(C.byref(r), C.byref(b), None) == -1
+    assert lib.fac_conv_nd_dual(C.byref(desc(96, 28, 1)), C.byref(b), None) == -2  # cin % 64
+    assert lib.fac_conv_nd_dual(C.byref(a), C.byref(desc(256, 56, 1)), None) == -2  # 56x56 vs 28x28 outputs
+    assert lib.fac_conv_nd_dual(C.byref(a), C.byref(desc(256, 56, 2, cout=128)), None) == -2  # cout differs
+
+
 def test_state_dict_is_the_reference_layout(golden):
     from fac_fake_amd.cvit import CViT
     want = list(golden("weights_checksums.json"))
