@@ -117,7 +117,7 @@ __device__ unsigned long long nd_ev[8][8][4];  // per wave: entry, prologue done
 // tap) tracking or per-piece branches (the generic path's VALU work was ~8.5
 // instructions per MFMA on the ResNet-50 layers in a round-3 SQ_INSTS_VALU pass).
 //
-// IL (interleaved issue, UT only): the next stage's glds pieces are issued
+// IL (interleaved issue): the next stage's glds pieces are issued
 // one at a time between the step's MFMA groups instead of all at the step
 // start.  A CU's TA takes ~1.3k cycles for the 48 KB of a 256 x 128 stage,
 // and issued in one block by all 8 waves at once (lock-step after the
@@ -194,9 +194,23 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
   int uc = 0, uz = 0, uy = 0, ux = 0;
   const long long rowstride = (long long)p.W * p.C8 * 8, planestride = rowstride * p.H;
 
-  // UT: glds piece q (A pieces 0..NA-1, then B) of stage st at the step state (uz, uy, ux, uc)
+  // glds piece q (A pieces 0..NA-1, then B) of stage st at the step state
+  // (UT: the wave-uniform (uz, uy, ux, uc); else this lane's tracked piece t)
   auto ut_piece = [&](int st, int q) {
     uint16_t* slot = smem + (st % NS) * SLOT;
+    if constexpr (!UT) {
+      if (q < NA) {
+        const bool real = st < p.ksteps && t.kp < p.ktot8;
+        const int iz = riz[q] + t.tz, iy = riy[q] + t.ty, ix = rix[q] + t.tx;
+        const bool ok = real && (unsigned)iz < (unsigned)p.D && (unsigned)iy < (unsigned)p.H &&
+                        (unsigned)ix < (unsigned)p.W;
+        const uint16_t* src = ok ? rbase[q] + (((size_t)iz * p.H + iy) * p.W + ix) * p.C8 * 8 + t.c8 * 8 : g_zero16;
+        glds16(src, slot + (NW * q + wave) * 64 * 8);
+      } else {
+        glds16(st < p.ksteps ? wsrc[q - NA] + (size_t)st * BK : g_zero16, slot + SLOT_A + (NW * (q - NA) + wave) * 64 * 8);
+      }
+      return;
+    }
     const bool real = st < p.ksteps;
     if (q < NA) {
       const long long toff = uz * planestride + uy * rowstride + (long long)ux * p.C8 * 8 + uc;
@@ -209,6 +223,12 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void convnd_igemm(ConvP p) {
     }
   };
   auto ut_advance = [&] {
+    if constexpr (!UT) {
+      t.kp += 8;
+      t.c8 += 8;
+      trk_norm(t, p.C8, p.KH, p.KW);
+      return;
+    }
     uc += 64;
     if (uc == p.C8 * 8) {
       uc = 0;
@@ -1786,11 +1806,16 @@ static hipError_t launch_convnd(ConvP p, int cout_pad, hipStream_t st) {
     const char* e = std::getenv("FAC_ND_IL");
     return !(e && e[0] == '0');
   }();
+  static const bool il_g = [] {
+    const char* e = std::getenv("FAC_ND_IL_G");  // interleaved issue on the general (per-lane tap) gather too
+    return !(e && e[0] == '0');
+  }();
   if (ut_on && p.C8 % 8 == 0) {
     if (il_on) launch_convnd_t<T, true, true>(p, st);
     else launch_convnd_t<T, true, false>(p, st);
   } else {
-    launch_convnd_t<T, false, false>(p, st);
+    if (il_on && il_g) launch_convnd_t<T, false, true>(p, st);
+    else launch_convnd_t<T, false, false>(p, st);
   }
   return hipGetLastError();
 }
