@@ -10,7 +10,9 @@ for rep in 1 2; do
 import json, sys
 d = json.loads(open("gpurun_out/arm.log").read().strip().splitlines()[-1])
 st = d["stage_ms"]
-print(f"[{sys.argv[1]:16s}] {d['value']:9.1f} crops/s  {d['ms_per_step']:.3f} ms  conv4-6 {st['conv4']:.3f} {st['conv5']:.3f} {st['conv6']:.3f}", flush=True)
+g = lambda a, b: sum(st[f"conv{i}"] for i in range(a, b + 1))
+print(f"[{sys.argv[1]:16s}] {d['value']:9.1f} crops/s  {d['ms_per_step']:.3f} ms  conv4-6 {g(4, 6):.3f} "
+      f"56^2 {g(7, 9):.3f} 28^2 {g(10, 13):.3f} 14^2 {g(14, 17):.3f}", flush=True)
 PY
   done
 done
