@@ -902,6 +902,160 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const uint16_t* __restrict__
   }
 }
 
+// ---- conv_s2d4_mp: conv_s2d4 (+ bias + ReLU) with the MaxPool2d(3, 2, 1)
+// that follows it in ResNet-50 (ResVitKan.py:187's torchvision resnet50:
+// conv1 -> bn1 -> relu -> maxpool) fused in, so the 112^2 conv output never
+// goes through HBM (4x the pooled bytes written, then read back by
+// fac_pool_nd).  A box is 4 x 14 pooled outputs = conv rows 2py0-1 .. 2py0+7
+// and columns 2px0-1 .. 2px0+27 (9 x 29, the one-row / one-column overlap
+// with the neighbouring boxes recomputed: 1.29x the MFMAs of the conv alone).
+// MFMA tile (r, h) = conv row r of the box, columns 16h .. 16h+15 (the three
+// past column 28 recompute column 28 and are dropped): wave (wm = h, wn)
+// holds its 8 channels of one column for all 9 rows, so the vertical 3-max
+// of the pool is fmaxf in registers; the vertically pooled rows (16-bit: a
+// max of rounded values is the rounded max, rounding being monotone) go
+// through a 4 x 32-column LDS stage for the horizontal 3-max and leave as
+// 16-byte stores.  Pool padding (conv row / column -1 at the image's top /
+// left edge) counts as 0, which never wins over a ReLU output, i.e. is
+// ignored as MaxPool2d ignores it -- hence relu is required.
+template <class T>
+__global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                       const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                       int nbox, int Hc, int Wc, int Hp, int Wp, int kp) {
+  constexpr int PH = 4, PW = 14;                     // pooled outputs per box
+  constexpr int CR = 2 * PH + 1, CC = 2 * PW + 1;    // conv rows / columns per box (9 x 29)
+  constexpr int HH = CR + 3, RPX = 32;               // halo rows, row pitch (cells: columns 0 .. CC + 2)
+  constexpr int HSL = 2 * HH * RPX;                  // 16-byte halo slots
+  constexpr int HPW = (HSL + 255) / 256;             // glds per wave
+  constexpr int WEL = 64 * 256;                      // weight elements
+  constexpr int HEL = HPW * 256 * 8;                 // halo buffer elements
+  constexpr int VP = 64 + 8;                         // stage pitch per column (elements)
+  constexpr int VEL = PH * 32 * VP;                  // vertically pooled stage [py][column][64]
+  static_assert(CC - 1 + 3 < RPX && HSL % 256 == 0, "halo geometry");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * HEL + VEL];
+  uint16_t* const sw = smem;
+  uint16_t* const vst = smem + WEL + 2 * HEL;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int wm = wave >> 1, wn = wave & 1;  // wm: column half of the box
+
+  // weights as conv_s2d4 (channel-permuted rows: lane group g ends with
+  // channels 32wn + 8g .. +7 of its column)
+  for (int c = tid; c < 64 * 32; c += 256) {
+    const int n = c >> 5, k8 = c & 31;
+    const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
+    *(u16x8*)(sw + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) =
+        *(const u16x8*)(w + (size_t)n * kp + k8 * 8);
+  }
+  float bv[2][4];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[32 * wn + 8 * g + 4 * ct + j] : 0.f;
+  const int col = 16 * wm + r16, colc = col < CC ? col : CC - 1;
+  int bo[CR];  // halo slot of tile r at tap (0, g/2)
+#pragma unroll
+  for (int r = 0; r < CR; ++r) bo[r] = ((g & 1) * HH + r) * RPX + colc + (g >> 1);
+  const int bpr = Wp / PW, bpi = (Hp / PH) * bpr;
+  auto issue = [&](int bx, uint16_t* halo) {
+    const int img = bx / bpi, rr = bx - img * bpi;
+    const int cy0 = (rr / bpr) * 2 * PH - 1, cx0 = (rr - (rr / bpr) * bpr) * 2 * PW - 1;
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const int sl = (i * 4 + wave) * 64 + lane;
+      const int pc = sl / (HH * RPX), rem = sl - pc * (HH * RPX), hy = rem / RPX, hx = rem - (rem / RPX) * RPX;
+      const int y = cy0 + hy, x = cx0 + hx;
+      const uint16_t* src = g_zero16;
+      if ((unsigned)y < (unsigned)Hc && (unsigned)x < (unsigned)Wc)
+        src = in + (((size_t)img * Hc + y) * Wc + x) * 16 + pc * 8;
+      glds16(src, halo + (i * 4 + wave) * 64 * 8);
+    }
+  };
+  // stores per thread of a box's horizontal pass: waves whose threads all
+  // have a second item issue 2, the rest 1 (counted in the halo wait below)
+  constexpr int NIT = PH * PW * 8;
+  static_assert(NIT > 256 && NIT <= 512 && (NIT - 256) % 64 == 0, "two store rounds, wave-uniform");
+  const bool two = tid + 256 < NIT;
+  __syncthreads();  // weights in
+  if (blockIdx.x < nbox) issue(blockIdx.x, smem + WEL);
+  int it = 0;
+  for (int bx = blockIdx.x; bx < nbox; bx += gridDim.x, ++it) {
+    const int img = bx / bpi, rr = bx - img * bpi;
+    const int py0 = (rr / bpr) * PH, px0 = (rr - (rr / bpr) * bpr) * PW;
+    uint16_t* const halo = smem + WEL + (it & 1) * HEL;
+    const bool more = bx + (int)gridDim.x < nbox;
+    // every wave is done with the other halo buffer and with the stage
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (more) issue(bx + gridDim.x, smem + WEL + ((it + 1) & 1) * HEL);
+    // this box's halo landed; younger: the next box's pieces (if any) and,
+    // after the first box, the previous box's 1 or 2 stores
+    if (it == 0) {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    } else if (two) {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW + 2) : "memory");
+      else asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    } else {
+      if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW + 1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(1)\n\ts_barrier" ::: "memory");
+    }
+    f32x4 acc[CR][2];
+#pragma unroll
+    for (int r = 0; r < CR; ++r) acc[r][0] = acc[r][1] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u16x8 wf[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(sw + (((s * 4 + 2 * wn + ct) * 4 + g) * 16 + r16) * 8);
+      const int so = (s >> 1) * RPX + (s & 1) * 2;
+#pragma unroll
+      for (int r = 0; r < CR; ++r) {
+        const u16x8 pf = *(const u16x8*)(halo + (bo[r] + so) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[r][ct] = T::mfma(wf[ct], pf, acc[r][ct]);
+      }
+    }
+    // vertical 3-max (row 0 is conv row -1, pool padding, at the top edge)
+    const bool top = py0 == 0;
+#pragma unroll
+    for (int py = 0; py < PH; ++py) {
+      u16x4 q[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float a = relu(acc[2 * py][ct][j] + bv[ct][j]);
+          if (py == 0 && top) a = 0.f;
+          const float b = relu(acc[2 * py + 1][ct][j] + bv[ct][j]);
+          const float c = relu(acc[2 * py + 2][ct][j] + bv[ct][j]);
+          v[j] = fmaxf(fmaxf(a, b), c);
+        }
+        q[ct] = T::pack4(v);
+      }
+      *(u16x8*)(vst + (py * 32 + col) * VP + 32 * wn + 8 * g) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // horizontal 3-max (column 0 is conv column -1 at the left edge) + store
+    const bool left = px0 == 0;
+    for (int k = tid; k < NIT; k += 256) {
+      const int q8 = k & 7, pj = k >> 3, py = pj / PW, j = pj - py * PW;
+      const uint16_t* v = vst + (py * 32 + 2 * j) * VP + q8 * 8;
+      const u16x8 a = *(const u16x8*)v, b = *(const u16x8*)(v + VP), c = *(const u16x8*)(v + 2 * VP);
+      const bool skip_a = left && j == 0;
+      f32x4 lo, hi;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        lo[e] = fmaxf(fmaxf(skip_a ? 0.f : T::to_f32(a[e]), T::to_f32(b[e])), T::to_f32(c[e]));
+        hi[e] = fmaxf(fmaxf(skip_a ? 0.f : T::to_f32(a[e + 4]), T::to_f32(b[e + 4])), T::to_f32(c[e + 4]));
+      }
+      const u16x4 l4 = T::pack4(lo), h4 = T::pack4(hi);
+      *(u16x8*)(out + (((size_t)img * Hp + py0 + py) * Wp + px0 + j) * 64 + q8 * 8) =
+          __builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+}
+
 
 // ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128, 256} — ResNet-50's
 // bottleneck expansions (conv3 64 -> 256 / 128 -> 512 + residual + ReLU,
@@ -1894,16 +2048,34 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
   const bool split = split1 < d->cout;
   if (split) p.vec_out = p.vec_out && ldo1 % 8 == 0 && ldo2 % 8 == 0;
   hipStream_t st = (hipStream_t)stream;
-  // the space-to-depth first conv (4x4/1 over 16-channel cells, cout 64, no
-  // residual, dense output): its own kernel (conv_s2d4)
-  if (!split && d->kd == 1 && d->kh == 4 && d->kw == 4 && d->sd == 1 && d->sh == 1 && d->sw == 1 && d->pd == 0 && d->ph == 0 &&
-      d->pw == 0 && d->cin == 16 && d->cout == 64 && k_pad == 256 && d->oh % 8 == 0 && d->ow % 28 == 0 &&
-      d->ldo == 64 && d->c_off == 0 && (d->flags & ~FAC_CONV_RELU) == 0) {
-    const int nimg = d->n * d->od, nbox = nimg * (d->oh / 8) * (d->ow / 28);
+  const bool s2d4_shape = !split && d->kd == 1 && d->kh == 4 && d->kw == 4 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+                          d->pd == 0 && d->ph == 0 && d->pw == 0 && d->cin == 16 && d->cout == 64 && k_pad == 256 &&
+                          d->oh % 8 == 0 && d->ow % 28 == 0 && d->ldo == 64 && d->c_off == 0;
+  auto cu_count = [] {
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
-    const int grid = std::min(nbox, 2 * ncu);  // two resident (two halo buffers + weights: 56 KB each)
+    return ncu;
+  };
+  // + MaxPool2d(3, 2, 1): only the space-to-depth first conv with ReLU
+  // (ResNet-50's conv1 -> bn1 -> relu -> maxpool), conv_s2d4_mp
+  if (d->flags & FAC_CONV_MAXPOOL3S2) {
+    if (!s2d4_shape || d->flags != (FAC_CONV_RELU | FAC_CONV_MAXPOOL3S2)) return FAC_ERR_ARG;
+    const int nimg = d->n * d->od, hp = d->oh / 2, wp = d->ow / 2, nbox = nimg * (hp / 4) * (wp / 14);
+    const int grid = std::min(nbox, 2 * cu_count());  // two resident (76 KB of LDS each)
+    if (d->dtype == FAC_DTYPE_BF16)
+      conv_s2d4_mp<BF16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
+                                               (uint16_t*)d->out, nbox, d->h, d->w, hp, wp, k_pad);
+    else
+      conv_s2d4_mp<F16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
+                                              (uint16_t*)d->out, nbox, d->h, d->w, hp, wp, k_pad);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  // the space-to-depth first conv (4x4/1 over 16-channel cells, cout 64, no
+  // residual, dense output): its own kernel (conv_s2d4)
+  if (s2d4_shape && (d->flags & ~FAC_CONV_RELU) == 0) {
+    const int nimg = d->n * d->od, nbox = nimg * (d->oh / 8) * (d->ow / 28);
+    const int grid = std::min(nbox, 2 * cu_count());  // two resident (two halo buffers + weights: 56 KB each)
     const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
     if (d->dtype == FAC_DTYPE_BF16)
       conv_s2d4<BF16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,

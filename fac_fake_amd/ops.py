@@ -19,7 +19,7 @@ from . import _lib
 
 TORCH16 = {"bf16": torch.bfloat16, "fp16": torch.float16}
 
-RELU, RESID, RELU2, OUT_F32 = 1, 2, 4, 8   # FAC_CONV_* epilogue flags
+RELU, RESID, RELU2, OUT_F32, MAXPOOL3S2 = 1, 2, 4, 8, 16   # FAC_CONV_* epilogue flags
 
 
 class ConvDesc(ctypes.Structure):
@@ -179,19 +179,27 @@ class ConvLayer:
                 (w + 2 * g.pw - g.kw) // g.sw + 1)
 
     def __call__(self, x: torch.Tensor, *, relu: bool = True, out: torch.Tensor | None = None, c_off: int = 0,
-                 residual: torch.Tensor | None = None, relu2: bool = False, out_f32: bool = False) -> torch.Tensor:
+                 residual: torch.Tensor | None = None, relu2: bool = False, out_f32: bool = False,
+                 maxpool3s2: bool = False) -> torch.Tensor:
+        """maxpool3s2: MaxPool2d(3, 2, 1) over H, W fused into the launch
+        (FAC_CONV_MAXPOOL3S2: the space-to-depth first conv with relu only;
+        the output is the pooled [N, D, Ho/2, Wo/2, C])."""
         n, d, h, w, c = x.shape
         if c != self.cin_p or x.dtype != TORCH16[self.dtype] or not x.is_contiguous():
             raise ValueError(f"conv input must be contiguous {self.dtype} [N,D,H,W,{self.cin_p}], got "
                              f"{x.dtype} {tuple(x.shape)}")
         od, oh, ow = self.out_dims(d, h, w)
+        if maxpool3s2:
+            if not relu or residual is not None or relu2 or out_f32 or c_off or oh % 2 or ow % 2:
+                raise ValueError("maxpool3s2 needs relu, no residual / relu2 / fp32 output, even output dims")
+            oh, ow = oh // 2, ow // 2
         if out is None:
             out = torch.empty(n, od, oh, ow, self.cout, device=x.device,
                               dtype=torch.float32 if out_f32 else x.dtype)
         if tuple(out.shape[:4]) != (n, od, oh, ow) or not out.is_contiguous():
             raise ValueError(f"conv output must be contiguous [{n},{od},{oh},{ow},C], got {tuple(out.shape)}")
         if (self._w33 is not None and h == w and residual is None and not relu2 and not out_f32 and c_off == 0
-                and out.shape[4] == self.cout):
+                and not maxpool3s2 and out.shape[4] == self.cout):
             pk = self._packed33(h)
             if pk is not None:
                 lib = _lib.load()
@@ -208,9 +216,10 @@ class ConvLayer:
         dsc.cout, dsc.k_pad = self.cout, self.k_pad
         dsc.kd, dsc.kh, dsc.kw, dsc.sd, dsc.sh, dsc.sw = g.kd, g.kh, g.kw, g.sd, g.sh, g.sw
         dsc.pd, dsc.ph, dsc.pw = g.pd, g.ph, g.pw
-        dsc.od, dsc.oh, dsc.ow = od, oh, ow
+        dsc.od, dsc.oh, dsc.ow = (od, 2 * oh, 2 * ow) if maxpool3s2 else (od, oh, ow)
         dsc.out, dsc.ldo, dsc.c_off = out.data_ptr(), out.shape[4], c_off
-        flags = (RELU if relu else 0) | (RELU2 if relu2 else 0) | (OUT_F32 if out_f32 else 0)
+        flags = (RELU if relu else 0) | (RELU2 if relu2 else 0) | (OUT_F32 if out_f32 else 0) | \
+            (MAXPOOL3S2 if maxpool3s2 else 0)
         if residual is not None:
             if tuple(residual.shape[:4]) != (n, od, oh, ow) or residual.dtype != x.dtype:
                 raise ValueError("residual must match the output positions and dtype")

@@ -189,6 +189,9 @@ class ResVitKan(nn.Module):
     feature_chunk = 0
     side_downsample = os.environ.get("FAC_RVK_SIDE", "1") != "0"
     fuse_downsample = os.environ.get("FAC_RVK_DUAL", "1") != "0"
+    # conv1 + bn1 + relu + maxpool as one launch (conv_s2d4_mp); FAC_RVK_MP=0:
+    # conv_s2d4 then fac_pool_nd
+    fuse_maxpool = os.environ.get("FAC_RVK_MP", "1") != "0"
 
     def _side_stream(self, device: torch.device):
         st = getattr(self, "_side", None)
@@ -209,8 +212,12 @@ class ResVitKan(nn.Module):
         step = B if taps is not None else (self.feature_chunk or B)
         tap = taps.append if taps is not None else (lambda t: None)
         for b0 in range(0, B, step):
-            x = self._conv1(x16[b0:b0 + step])                      # 7x7/2 + bn1 + ReLU, on s2d cells
-            x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))    # MaxPool2d(3, 2, 1)
+            if self.fuse_maxpool:
+                # 7x7/2 + bn1 + ReLU + MaxPool2d(3, 2, 1) in one launch (conv_s2d4_mp)
+                x = self._conv1(x16[b0:b0 + step], maxpool3s2=True)
+            else:
+                x = self._conv1(x16[b0:b0 + step])                  # 7x7/2 + bn1 + ReLU, on s2d cells
+                x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))  # MaxPool2d(3, 2, 1)
             tap(x)
             for c1, c2, c3, ds in self._blocks:
                 if ds is not None and self.fuse_downsample:

@@ -28,6 +28,12 @@ extern "C" {
 #define FAC_CONV_RESID 2     /* v = v + residual[m][r_off + c] (16-bit) */
 #define FAC_CONV_RELU2 4     /* v = max(v, 0) after the residual */
 #define FAC_CONV_OUT_F32 8   /* fp32 output instead of 16-bit */
+#define FAC_CONV_MAXPOOL3S2 16 /* then MaxPool2d(3, 2, 1) over H, W: out is
+                                [n][od][oh/2][ow/2][ldo]; only with
+                                FAC_CONV_RELU alone, on the space-to-depth
+                                first conv below (ResNet-50's conv1 + bn1 +
+                                relu + maxpool, ResVitKan.py:187/205);
+                                FAC_ERR_ARG otherwise */
 
 /* One N-d convolution (Conv2d / Conv3d, any kernel, stride, zero padding,
  * dilation 1, groups 1) with folded BatchNorm, as an implicit GEMM on MFMA:

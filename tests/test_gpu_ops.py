@@ -95,6 +95,34 @@ def test_conv_nd_vs_torch_fp32(case, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("n,d,h,w", [(2, 1, 19, 59), (1, 2, 35, 31), (3, 1, 115, 115)])
+def test_conv_s2d4_maxpool_fused(n, d, h, w, dt):
+    """conv_s2d4_mp (FAC_CONV_MAXPOOL3S2): the 4x4/1 space-to-depth conv +
+    bias + ReLU + MaxPool2d(3, 2, 1) in one launch is bit-identical to
+    conv_s2d4 followed by fac_pool_nd (a max selects one of its inputs, and
+    rounding is monotone), and within one 16-bit ulp of torch's fp32 conv ->
+    relu -> rounded -> max_pool.  Every box touches the top or left pool
+    padding on the first row / column of boxes; biases straddle 0 so ReLU
+    zeros occur."""
+    from fac_fake_amd.ops import ConvLayer, max_pool_sep
+    g = torch.Generator().manual_seed(7 + h + d)
+    x = torch.randn(n, 16, d, h, w, generator=g).to(T16[dt]).float()
+    wt = (torch.randn(64, 16, 1, 4, 4, generator=g) / 16).float()
+    b = torch.randn(64, generator=g) * 0.5
+    layer = ConvLayer(wt, b, 1, 0, dtype=dt, device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    fused = layer(xg, relu=True, maxpool3s2=True)
+    unf = max_pool_sep(layer(xg, relu=True), (1, 3, 3), (1, 2, 2), (0, 1, 1))
+    torch.cuda.synchronize()
+    assert tuple(fused.shape) == (n, d, (h - 3) // 2, (w - 3) // 2, 64)
+    assert torch.equal(fused.cpu(), unf.cpu())
+    conv = F.relu(F.conv3d(x, wt.to(T16[dt]).float(), b)).to(T16[dt]).float()
+    ref = F.max_pool3d(conv, (1, 3, 3), (1, 2, 2), (0, 1, 1)).permute(0, 2, 3, 4, 1).to(T16[dt])
+    u = _ulps(fused.cpu(), ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("cin,cout", [(64, 256), (128, 512), (256, 1024), (256, 64)])
 def test_conv_pw_residual_into_slot(cin, cout, dt):
     """conv_pw's bottleneck epilogue relu(relu(conv + b) + res) written into

@@ -80,6 +80,33 @@ def test_conv_nd_dual_argument_checks(built_lib):
     assert lib.fac_conv_nd_dual(C.byref(a), C.byref(desc(256, 56, 2, cout=128)), None) == -2  # cout differs
 
 
+def test_conv_maxpool_flag_argument_checks(built_lib):
+    """FAC_CONV_MAXPOOL3S2 is only accepted on the space-to-depth first conv
+    with FAC_CONV_RELU alone; anything else is FAC_ERR_ARG, returned before
+    any launch."""
+    import ctypes as C
+    from fac_fake_amd import _lib
+    from fac_fake_amd.ops import ConvDesc, MAXPOOL3S2, RELU, RESID
+    lib = _lib.load()
+
+    def desc(kh=4, cin=16, cout=64, h=115, flags=RELU | MAXPOOL3S2):
+        d = ConvDesc()
+        d.dtype, d.inp, d.weight, d.out = 0, 16, 16, 16
+        d.n, d.d, d.h, d.w, d.cin, d.cout = 2, 1, h, h, cin, cout
+        d.kd, d.kh, d.kw = 1, kh, kh
+        d.sd = d.sh = d.sw = 1
+        d.od, d.oh, d.ow = 1, h - kh + 1, h - kh + 1
+        d.k_pad = (kh * kh * cin + 63) // 64 * 64
+        d.ldo, d.flags = cout, flags
+        return d
+
+    assert lib.fac_conv_nd(C.byref(desc(flags=MAXPOOL3S2)), None) == -1            # no ReLU
+    assert lib.fac_conv_nd(C.byref(desc(flags=RELU | RESID | MAXPOOL3S2)), None) == -1
+    assert lib.fac_conv_nd(C.byref(desc(kh=3, cin=64)), None) == -1                # not the s2d conv
+    assert lib.fac_conv_nd(C.byref(desc(cout=128)), None) == -1
+    assert lib.fac_conv_nd(C.byref(desc(h=60)), None) == -1                        # 57 outputs: no 8 x 28 boxes
+
+
 def test_state_dict_is_the_reference_layout(golden):
     from fac_fake_amd.cvit import CViT
     want = list(golden("weights_checksums.json"))
