@@ -907,23 +907,25 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const uint16_t* __restrict__
 // conv1 -> bn1 -> relu -> maxpool) fused in, so the 112^2 conv output never
 // goes through HBM (4x the pooled bytes written, then read back by
 // fac_pool_nd).  A box is 4 x 14 pooled outputs = conv rows 2py0-1 .. 2py0+7
-// and columns 2px0-1 .. 2px0+27 (9 x 29, the one-row / one-column overlap
-// with the neighbouring boxes recomputed: 1.29x the MFMAs of the conv alone).
-// MFMA tile (r, h) = conv row r of the box, columns 16h .. 16h+15 (the three
-// past column 28 recompute column 28 and are dropped): wave (wm = h, wn)
-// holds its 8 channels of one column for all 9 rows, so the vertical 3-max
-// of the pool is fmaxf in registers; the vertically pooled rows (16-bit: a
-// max of rounded values is the rounded max, rounding being monotone) go
-// through a 4 x 32-column LDS stage for the horizontal 3-max and leave as
-// 16-byte stores.  Pool padding (conv row / column -1 at the image's top /
-// left edge) counts as 0, which never wins over a ReLU output, i.e. is
-// ignored as MaxPool2d ignores it -- hence relu is required.
+// and columns 2px0-1 .. 2px0+27.  A workgroup walks whole column strips of an
+// image top to bottom, so conv row 2py0-1 is the previous box's last row,
+// kept in registers (at the top edge it is pool padding): each box computes
+// the 8 rows 2py0 .. 2py0+7 only.  MFMA tile (r, h) = conv row r of those,
+// columns 16h .. 16h+15 (the three past column 28 recompute column 28 and are
+// dropped; 1.14x the MFMAs of the conv alone): wave (wm = h, wn) holds its 8
+// channels of one column for all rows, so the vertical 3-max of the pool is
+// fmaxf in registers; the vertically pooled rows (16-bit: a max of rounded
+// values is the rounded max, rounding being monotone) go through a 4 x
+// 32-column LDS stage for the horizontal 3-max and leave as 16-byte stores.
+// Pool padding (conv row / column -1 at the image's top / left edge) counts
+// as 0, which never wins over a ReLU output, i.e. is ignored as MaxPool2d
+// ignores it -- hence relu is required.
 template <class T>
 __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
                                                        const float* __restrict__ bias, uint16_t* __restrict__ out,
-                                                       int nbox, int Hc, int Wc, int Hp, int Wp, int kp) {
+                                                       int nstrip, int Hc, int Wc, int Hp, int Wp, int kp) {
   constexpr int PH = 4, PW = 14;                     // pooled outputs per box
-  constexpr int CR = 2 * PH + 1, CC = 2 * PW + 1;    // conv rows / columns per box (9 x 29)
+  constexpr int CR = 2 * PH, CC = 2 * PW + 1;        // conv rows computed / columns needed per box (8 x 29)
   constexpr int HH = CR + 3, RPX = 32;               // halo rows, row pitch (cells: columns 0 .. CC + 2)
   constexpr int HSL = 2 * HH * RPX;                  // 16-byte halo slots
   constexpr int HPW = (HSL + 255) / 256;             // glds per wave
@@ -931,7 +933,7 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
   constexpr int HEL = HPW * 256 * 8;                 // halo buffer elements
   constexpr int VP = 64 + 8;                         // stage pitch per column (elements)
   constexpr int VEL = PH * 32 * VP;                  // vertically pooled stage [py][column][64]
-  static_assert(CC - 1 + 3 < RPX && HSL % 256 == 0, "halo geometry");
+  static_assert(CC - 1 + 3 < RPX, "halo geometry");
   __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * HEL + VEL];
   uint16_t* const sw = smem;
   uint16_t* const vst = smem + WEL + 2 * HEL;
@@ -956,17 +958,26 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
   int bo[CR];  // halo slot of tile r at tap (0, g/2)
 #pragma unroll
   for (int r = 0; r < CR; ++r) bo[r] = ((g & 1) * HH + r) * RPX + colc + (g >> 1);
-  const int bpr = Wp / PW, bpi = (Hp / PH) * bpr;
-  auto issue = [&](int bx, uint16_t* halo) {
-    const int img = bx / bpi, rr = bx - img * bpi;
-    const int cy0 = (rr / bpr) * 2 * PH - 1, cx0 = (rr - (rr / bpr) * bpr) * 2 * PW - 1;
+  const int bpr = Wp / PW, nby = Hp / PH;
+  // k-th box of this workgroup: strip blockIdx.x + (k / nby) * gridDim.x, box row k % nby
+  auto box_of = [&](int k, int& img, int& py0, int& px0) {
+    const int s = blockIdx.x + (k / nby) * (int)gridDim.x;
+    img = s / bpr;
+    px0 = (s - img * bpr) * PW;
+    py0 = (k - (k / nby) * nby) * PH;
+    return s < nstrip;
+  };
+  auto issue = [&](int k, uint16_t* halo) {
+    int img, py0, px0;
+    box_of(k, img, py0, px0);
+    const int cy0 = 2 * py0, cx0 = 2 * px0 - 1;  // cell (= conv) row of box row 0, column of column 0
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
       const int sl = (i * 4 + wave) * 64 + lane;
       const int pc = sl / (HH * RPX), rem = sl - pc * (HH * RPX), hy = rem / RPX, hx = rem - (rem / RPX) * RPX;
       const int y = cy0 + hy, x = cx0 + hx;
       const uint16_t* src = g_zero16;
-      if ((unsigned)y < (unsigned)Hc && (unsigned)x < (unsigned)Wc)
+      if (pc < 2 && (unsigned)y < (unsigned)Hc && (unsigned)x < (unsigned)Wc)
         src = in + (((size_t)img * Hc + y) * Wc + x) * 16 + pc * 8;
       glds16(src, halo + (i * 4 + wave) * 64 * 8);
     }
@@ -976,20 +987,23 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
   constexpr int NIT = PH * PW * 8;
   static_assert(NIT > 256 && NIT <= 512 && (NIT - 256) % 64 == 0, "two store rounds, wave-uniform");
   const bool two = tid + 256 < NIT;
+  float carry[2][4];  // the previous box's last conv row (ReLU'd) of this lane's column
   __syncthreads();  // weights in
-  if (blockIdx.x < nbox) issue(blockIdx.x, smem + WEL);
-  int it = 0;
-  for (int bx = blockIdx.x; bx < nbox; bx += gridDim.x, ++it) {
-    const int img = bx / bpi, rr = bx - img * bpi;
-    const int py0 = (rr / bpr) * PH, px0 = (rr - (rr / bpr) * bpr) * PW;
-    uint16_t* const halo = smem + WEL + (it & 1) * HEL;
-    const bool more = bx + (int)gridDim.x < nbox;
+  {
+    int i0, y0, x0;
+    if (box_of(0, i0, y0, x0)) issue(0, smem + WEL);
+  }
+  int img, py0, px0;
+  for (int k = 0; box_of(k, img, py0, px0); ++k) {
+    uint16_t* const halo = smem + WEL + (k & 1) * HEL;
+    int i1, y1, x1;
+    const bool more = box_of(k + 1, i1, y1, x1);
     // every wave is done with the other halo buffer and with the stage
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (more) issue(bx + gridDim.x, smem + WEL + ((it + 1) & 1) * HEL);
+    if (more) issue(k + 1, smem + WEL + ((k + 1) & 1) * HEL);
     // this box's halo landed; younger: the next box's pieces (if any) and,
     // after the first box, the previous box's 1 or 2 stores
-    if (it == 0) {
+    if (k == 0) {
       if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     } else if (two) {
@@ -1015,8 +1029,13 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
         for (int ct = 0; ct < 2; ++ct) acc[r][ct] = T::mfma(wf[ct], pf, acc[r][ct]);
       }
     }
-    // vertical 3-max (row 0 is conv row -1, pool padding, at the top edge)
-    const bool top = py0 == 0;
+    // vertical 3-max over conv rows 2py0-1+2py .. +2: the carried row first
+    if (py0 == 0) {
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) carry[ct][j] = 0.f;  // pool padding
+    }
 #pragma unroll
     for (int py = 0; py < PH; ++py) {
       u16x4 q[2];
@@ -1025,11 +1044,10 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
         f32x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float a = relu(acc[2 * py][ct][j] + bv[ct][j]);
-          if (py == 0 && top) a = 0.f;
-          const float b = relu(acc[2 * py + 1][ct][j] + bv[ct][j]);
-          const float c = relu(acc[2 * py + 2][ct][j] + bv[ct][j]);
-          v[j] = fmaxf(fmaxf(a, b), c);
+          const float b = relu(acc[2 * py][ct][j] + bv[ct][j]);
+          const float c = relu(acc[2 * py + 1][ct][j] + bv[ct][j]);
+          v[j] = fmaxf(fmaxf(carry[ct][j], b), c);
+          carry[ct][j] = c;
         }
         q[ct] = T::pack4(v);
       }
@@ -1038,8 +1056,8 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     // horizontal 3-max (column 0 is conv column -1 at the left edge) + store
     const bool left = px0 == 0;
-    for (int k = tid; k < NIT; k += 256) {
-      const int q8 = k & 7, pj = k >> 3, py = pj / PW, j = pj - py * PW;
+    for (int it = tid; it < NIT; it += 256) {
+      const int q8 = it & 7, pj = it >> 3, py = pj / PW, j = pj - py * PW;
       const uint16_t* v = vst + (py * 32 + 2 * j) * VP + q8 * 8;
       const u16x8 a = *(const u16x8*)v, b = *(const u16x8*)(v + VP), c = *(const u16x8*)(v + 2 * VP);
       const bool skip_a = left && j == 0;
@@ -1055,7 +1073,6 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
     }
   }
 }
-
 
 // ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128, 256} — ResNet-50's
 // bottleneck expansions (conv3 64 -> 256 / 128 -> 512 + residual + ReLU,
@@ -2061,14 +2078,14 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
   // (ResNet-50's conv1 -> bn1 -> relu -> maxpool), conv_s2d4_mp
   if (d->flags & FAC_CONV_MAXPOOL3S2) {
     if (!s2d4_shape || d->flags != (FAC_CONV_RELU | FAC_CONV_MAXPOOL3S2)) return FAC_ERR_ARG;
-    const int nimg = d->n * d->od, hp = d->oh / 2, wp = d->ow / 2, nbox = nimg * (hp / 4) * (wp / 14);
-    const int grid = std::min(nbox, 2 * cu_count());  // two resident (76 KB of LDS each)
+    const int nimg = d->n * d->od, hp = d->oh / 2, wp = d->ow / 2, nstrip = nimg * (wp / 14);
+    const int grid = std::min(nstrip, 2 * cu_count());  // two resident (74 KB of LDS each)
     if (d->dtype == FAC_DTYPE_BF16)
       conv_s2d4_mp<BF16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
-                                               (uint16_t*)d->out, nbox, d->h, d->w, hp, wp, k_pad);
+                                               (uint16_t*)d->out, nstrip, d->h, d->w, hp, wp, k_pad);
     else
       conv_s2d4_mp<F16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
-                                              (uint16_t*)d->out, nbox, d->h, d->w, hp, wp, k_pad);
+                                              (uint16_t*)d->out, nstrip, d->h, d->w, hp, wp, k_pad);
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   // the space-to-depth first conv (4x4/1 over 16-channel cells, cout 64, no

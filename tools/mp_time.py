@@ -1,6 +1,9 @@
 """Time ResNet-50's conv1 (+ maxpool) at config 5's batch: conv_s2d4, fac_pool_nd,
 and the fused conv_s2d4_mp (FAC_CONV_MAXPOOL3S2), each over 20 back-to-back launches."""
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from fac_fake_amd.ops import ConvLayer, max_pool_sep
 
@@ -31,4 +34,4 @@ fused = t(lambda: layer(x, maxpool3s2=True))
 mb_in, mb_c, mb_p = x.numel() * 2 / 1e6, y.numel() * 2 / 1e6, y.numel() / 2 / 1e6
 fl = B * 112 * 112 * 64 * 256 * 2
 print(f"B={B}: conv_s2d4 {conv:.1f} us, pool {pool:.1f} us, sum {conv + pool:.1f}; fused {fused:.1f} us "
-      f"({(mb_in + mb_p) / fused * 1e-3:.2f} TB/s algorithmic, {fl / fused * 1e-6:.0f} TFLOP/s of the conv's FLOPs)")
+      f"({(mb_in + mb_p) / fused:.2f} TB/s algorithmic, {fl / fused * 1e-6:.0f} TFLOP/s of the conv's FLOPs)")
