@@ -181,7 +181,9 @@ def layer_roofline_ms(run, dtype: str) -> dict:
     downsample (ops.conv_dual) is one op whose bytes exclude the residual it
     no longer writes and reads.  The ResNet-50 and S3D layers
     at these batch sizes are mostly HBM-bound (arithmetic intensity under the
-    ~312 FLOP/B ridge), so the MFMA-only fraction understates them."""
+    ~312 FLOP/B ridge), so the MFMA-only fraction understates them.
+    ResNet's conv1 with its fused max-pool (conv_s2d4_mp) likewise counts as
+    one op (the conv's FLOPs, the input and the pooled output's bytes)."""
     from fac_fake_amd import ops, resvitkan, s3d
     recs = []
     orig_call, orig_pool, orig_sep = ops.ConvLayer.__call__, ops.pool, ops.max_pool_sep
@@ -195,6 +197,8 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         flops = 2.0 * M * self.cout * self.g.kd * self.g.kh * self.g.kw * self.cin
         esz = 4 if kw.get("out_f32") else 2
         byts = 2.0 * x.numel() + esz * M * self.cout + (2.0 * M * self.cout if kw.get("residual") is not None else 0)
+        if kw.get("maxpool3s2"):   # conv + fused max-pool (conv_s2d4_mp): one op writing only the pooled map
+            byts = 2.0 * (x.numel() + out.numel())
         recs.append((flops, byts))
         return out
 
