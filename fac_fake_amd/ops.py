@@ -199,7 +199,7 @@ class ConvLayer:
         if tuple(out.shape[:4]) != (n, od, oh, ow) or not out.is_contiguous():
             raise ValueError(f"conv output must be contiguous [{n},{od},{oh},{ow},C], got {tuple(out.shape)}")
         if (self._w33 is not None and h == w and residual is None and not relu2 and not out_f32 and c_off == 0
-                and not maxpool3s2 and out.shape[4] == self.cout):
+                and not maxpool3s2 and out.shape[4] == self.cout and self.cin_p == self.cin):
             pk = self._packed33(h)
             if pk is not None:
                 lib = _lib.load()

@@ -36,6 +36,13 @@ BN_EPS = 1e-3   # BatchNorm3d(eps=1e-3) in BasicConv3d / SepConv3d (model.py:54,
 _BUFFERS = ("rmean", "rvar", "nbt")
 
 
+def _pad_rows(t: torch.Tensor, n: int) -> torch.Tensor:
+    """t with zero rows appended along dim 0 up to n rows."""
+    if t.shape[0] == n:
+        return t
+    return torch.cat([t, t.new_zeros((n - t.shape[0],) + tuple(t.shape[1:]))])
+
+
 def _init_tensor(shape, kind):
     if kind == "nbt":
         return torch.zeros((), dtype=torch.long)
@@ -137,10 +144,25 @@ class S3D(nn.Module):
                          for h in (f"{p}.branch0.0", f"{p}.branch1.0", f"{p}.branch2.0")]
                 merged = ConvLayer(torch.cat([h[0] for h in heads]), torch.cat([h[1] for h in heads]), 1, 0,
                                    dtype=dt, device=device)
+                # merged path below 14x14 (no conv.hip tile there): branch1.0 /
+                # branch2.0 outputs padded with zero channels to a multiple of
+                # 64 (zero weight rows and biases: relu(0) = 0), so the (1,3,3)
+                # convs reading them take K steps that each lie in one tap
+                # (convnd_igemm's uniform-tap gather)
+                p1, p2 = self._pad64(b1a, 1), self._pad64(b2a, 2)
+                merged_p = merged
+                if (p1, p2) != (b1a, b2a):
+                    hw = [heads[0][0], _pad_rows(heads[1][0], p1), _pad_rows(heads[2][0], p2)]
+                    hb = [heads[0][1], _pad_rows(heads[1][1], p1), _pad_rows(heads[2][1], p2)]
+                    merged_p = ConvLayer(torch.cat(hw), torch.cat(hb), 1, 0, dtype=dt, device=device)
+                b1, b2 = sep(f"{p}.branch1.1", 3, 1, 1), sep(f"{p}.branch2.1", 3, 1, 1)
                 self._layers.append(("mixed", dict(
-                    b0=bconv(f"{p}.branch0.0"), b1a=bconv(f"{p}.branch1.0"), b1=sep(f"{p}.branch1.1", 3, 1, 1),
-                    b2a=bconv(f"{p}.branch2.0"), b2=sep(f"{p}.branch2.1", 3, 1, 1), b3=bconv(f"{p}.branch3.1"),
+                    b0=bconv(f"{p}.branch0.0"), b1a=bconv(f"{p}.branch1.0"), b1=b1,
+                    b2a=bconv(f"{p}.branch2.0"), b2=b2, b3=bconv(f"{p}.branch3.1"),
+                    b1p=b1 if p1 == b1a else sep(f"{p}.branch1.1", 3, 1, 1, cin_pad=p1),
+                    b2p=b2 if p2 == b2a else sep(f"{p}.branch2.1", 3, 1, 1, cin_pad=p2),
                     heads=merged, head_splits=(b0, b0 + b1a), head_widths=(b1a, b2a),
+                    heads_p=merged_p, head_splits_p=(b0, b0 + p1), head_widths_p=(p1, p2),
                     widths=(b0, b1b, b2b, b3))))
         self._fc = ConvLayer(sd["fc.0.weight"], sd["fc.0.bias"], 1, 0, dtype=dt, device=device)
         self._prep = (idx, v)
@@ -156,6 +178,14 @@ class S3D(nn.Module):
     concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "0") == "1"
     # serial order: the three 1x1x1 heads as one column-split launch (ops.conv_split)
     merged_heads = os.environ.get("FAC_S3D_MERGED_HEADS", "1") == "1"
+    # channel padding of the merged heads' branch1.0 / branch2.0 outputs to a
+    # multiple of 64: 0 none, 1 branch1.0 when >= 64 channels, 2 both
+    pad64_level = int(os.environ.get("FAC_S3D_PAD64", "1"))
+
+    def _pad64(self, c: int, level: int) -> int:
+        if self.pad64_level < level or c % 64 == 0 or (level == 1 and c < 64):
+            return c
+        return (c + 63) // 64 * 64
 
     def _branch_streams(self, device: torch.device):
         """Three side streams (per device) for the Inception branches."""
@@ -190,13 +220,15 @@ class S3D(nn.Module):
             blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
             return out
         if not self.concurrent_branches:
-            s1, t1 = blk["b1"]
-            s2, t2 = blk["b2"]
+            sfx = "_p" if h < 14 else ""   # channel-padded heads (pad64_level) where no conv.hip tile exists
+            s1, t1 = blk["b1p" if sfx else "b1"]
+            s2, t2 = blk["b2p" if sfx else "b2"]
             # branch0 into its slot, branch1.0 / branch2.0 into their own
             # tensors: one launch (column-split GEMM) instead of three
-            h1 = torch.empty(n, d, h, w, blk["head_widths"][0], dtype=x.dtype, device=x.device)
-            h2 = torch.empty(n, d, h, w, blk["head_widths"][1], dtype=x.dtype, device=x.device)
-            conv_split(blk["heads"], x, blk["head_splits"], out, 0, h1, h2)
+            hws = blk["head_widths" + sfx]
+            h1 = torch.empty(n, d, h, w, hws[0], dtype=x.dtype, device=x.device)
+            h2 = torch.empty(n, d, h, w, hws[1], dtype=x.dtype, device=x.device)
+            conv_split(blk["heads" + sfx], x, blk["head_splits" + sfx], out, 0, h1, h2)
             t1(s1(h1), out=out, c_off=o1)
             t2(s2(h2), out=out, c_off=o2)
             blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
