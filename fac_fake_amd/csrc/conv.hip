@@ -555,6 +555,15 @@ static int conv_nbox() {
   return n;
 }
 
+// FAC_CONV_POOL112_OCC=4: the pooled 112^2 tile (conv6) at 4 workgroups per CU, as conv4/5
+static int conv_pool112_occ() {
+  static const int n = [] {
+    const char* e = std::getenv("FAC_CONV_POOL112_OCC");
+    return e ? std::atoi(e) : 2;
+  }();
+  return n;
+}
+
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                                 int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st,
@@ -564,7 +573,14 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
     case 224032: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
     // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
-    case 112064: launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 112064:
+      // the pooled tile (conv6) spills at 4 per CU (128 VGPRs): 2 per CU
+      // (same box: conv4-6 0.665 -> 0.60 ms; FAC_CONV_POOL112_OCC=4 restores)
+      if (pool && conv_pool112_occ() != 4)
+        launch_box<T, 16, 16, 64, 4, 1, 1, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      else
+        launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      break;
     case 56128:
       if (conv_nbox() == 2 && (B * 14) % 2 == 0) {
         if (launch_box<T, 8, 28, 128, 2, 2, 2, 1, true, true, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
