@@ -212,6 +212,15 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         recs.append((flops, 2.0 * (h.numel() + x.numel() + out.numel())))
         return out
 
+    orig_pw2 = ops.bottleneck_pw2
+
+    def pw2_hook(c3, h, res, c1):   # conv3 + the next conv1 (fac_bottleneck_pw2): one op, x written once
+        x, h1 = orig_pw2(c3, h, res, c1)
+        M = x.numel() // c3.cout
+        recs.append((2.0 * M * (c3.cout * c3.cin + c1.cout * c1.cin),
+                     2.0 * (h.numel() + res.numel() + x.numel() + h1.numel())))
+        return x, h1
+
     def pool_hook(x, *a, **kw):
         out = orig_pool(x, *a, **kw)
         if not in_sep[0]:
@@ -229,6 +238,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
 
     ops.ConvLayer.__call__ = conv_hook
     ops.conv_dual = resvitkan.conv_dual = dual_hook
+    ops.bottleneck_pw2 = resvitkan.bottleneck_pw2 = pw2_hook
     ops.pool = resvitkan.pool = s3d.pool = pool_hook
     resvitkan.max_pool_sep = s3d.max_pool_sep = sep_hook
     try:
@@ -237,6 +247,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
     finally:
         ops.ConvLayer.__call__ = orig_call
         ops.conv_dual = resvitkan.conv_dual = orig_dual
+        ops.bottleneck_pw2 = resvitkan.bottleneck_pw2 = orig_pw2
         ops.pool = resvitkan.pool = s3d.pool = orig_pool
         resvitkan.max_pool_sep = s3d.max_pool_sep = orig_sep
     peak = PEAK_TFLOPS[dtype] * 1e12

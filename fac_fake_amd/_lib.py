@@ -58,6 +58,7 @@ SIGNATURES = {
     # include/fac_ops.h
     "fac_conv_nd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "fac_conv_nd_dual": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "fac_bottleneck_pw2": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_conv_weight_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "fac_pool_nd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

@@ -1074,6 +1074,162 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
   }
 }
 
+// ---- bneck_pw2: a ResNet-50 layer1 bottleneck's conv3 (1x1, 64 -> 256,
+// + bn3 + ReLU + identity residual + ReLU, ResVitKan.py:146-152) and the
+// NEXT block's conv1 (1x1, 256 -> N1 + bn1 + ReLU) in one persistent launch:
+// a workgroup computes all 256 conv3 channels of a 64-row tile, stores them
+// (the next block's residual) and keeps them in LDS as the next conv1's K,
+// so the 256-channel map is not read back from HBM by a second launch.
+// Both GEMMs run transposed (rows = channels) with conv_pw's channel
+// permutation, so every lane stores 16 bytes (8 channels of one position)
+// straight from registers; the epilogue arithmetic is conv_pw's, and the
+// 16-bit conv3 outputs are exactly what the separate conv1 would read.
+// The next tile's A rows and residual block are loaded into registers while
+// the current tile computes.
+// Rows past M (a partial last tile) load row M-1 and store into g_sink, so
+// every load and store is unconditional: the compiler's wait for the next
+// tile's registers then counts this tile's stores instead of draining them.
+__device__ uint16_t g_sink[64 * 8];
+
+template <class T, int N1>
+__global__ __launch_bounds__(512, 1) void bneck_pw2(const uint16_t* __restrict__ a, const uint16_t* __restrict__ w3,
+                                                    const float* __restrict__ b3, const uint16_t* __restrict__ res,
+                                                    const uint16_t* __restrict__ w1, const float* __restrict__ b1,
+                                                    uint16_t* __restrict__ xo, uint16_t* __restrict__ ho, int M,
+                                                    int kp3, int kp1, int ldr, int r_off) {
+  constexpr int BM = 64, K3 = 64, C3 = 256, PPW = N1 / 64;  // rows per tile, conv3 K / N, conv1 channel pairs per wave
+  constexpr int W3EL = C3 * K3, W1EL = N1 * C3, AEL = BM * K3, XEL = BM * C3;
+  static_assert(N1 == 64 || N1 == 128, "conv1 width");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[W3EL + W1EL + AEL + XEL];
+  uint16_t* const s3 = smem;
+  uint16_t* const s1 = smem + W3EL;
+  uint16_t* const sa = s1 + W1EL;   // A tile: rows of 8 pieces, piece p at p ^ (row & 7)
+  uint16_t* const sx = sa + AEL;    // conv3 tile: rows of 32 pieces, piece q at q ^ (row & 15)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // W3 fragments [w][s][ct][g][r16][8]: row i of (wave w, tile ct) = channel
+  // 32w + 8(i>>2) + 4ct + (i&3); W1 fragments [P][s][h][g][r16][8] likewise
+  for (int c = tid; c < C3 * 8; c += 512) {
+    const int n = c >> 3, k8 = c & 7, nn = n & 31;
+    const int ct = (nn >> 2) & 1, i = 4 * ((nn >> 3) & 3) + (nn & 3);
+    *(u16x8*)(s3 + (((((n >> 5) * 2 + (k8 >> 2)) * 2 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) =
+        *(const u16x8*)(w3 + (size_t)n * kp3 + k8 * 8);
+  }
+  for (int c = tid; c < N1 * 32; c += 512) {
+    const int n = c >> 5, k8 = c & 31, nn = n & 31;
+    const int h = (nn >> 2) & 1, i = 4 * ((nn >> 3) & 3) + (nn & 3);
+    *(u16x8*)(s1 + (((((n >> 5) * 8 + (k8 >> 2)) * 2 + h) * 4 + (k8 & 3)) * 16 + i) * 8) =
+        *(const u16x8*)(w1 + (size_t)n * kp1 + k8 * 8);
+  }
+  float bv3[2][4], bv1[PPW][2][4];
+  const int pt2 = wave >> 1;  // conv1: this wave's position tile, channel pairs (wave & 1) * PPW + pp
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv3[ct][j] = b3[32 * wave + 8 * g + 4 * ct + j];
+#pragma unroll
+  for (int pp = 0; pp < PPW; ++pp)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv1[pp][h][j] = b1[32 * ((wave & 1) * PPW + pp) + 8 * g + 4 * h + j];
+
+  const int ntiles = (M + BM - 1) / BM;
+  const int arow = tid >> 3, apc = tid & 7;  // this thread's A piece of a tile
+  u16x8 an = (u16x8)0, rn[4], rc[4];
+  auto load = [&](int t) {
+    const int m0 = t * BM;
+    an = *(const u16x8*)(a + (size_t)min(m0 + arow, M - 1) * K3 + apc * 8);
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int m = min(m0 + pt * 16 + r16, M - 1);
+      rn[pt] = *(const u16x8*)(res + (size_t)m * ldr + r_off + 32 * wave + 8 * g);
+    }
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  __syncthreads();  // weights in
+  for (; t < ntiles; t += gridDim.x) {
+    const int m0 = t * BM;
+    // A tile into LDS (every wave finished the previous tile's conv3 reads of
+    // it before the previous tile's second barrier), next tile's loads out
+    *(u16x8*)(sa + (arow * 8 + (apc ^ (arow & 7))) * 8) = an;
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) rc[pt] = rn[pt];
+    if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // conv3: channels 32 wave + (2 tiles) x the tile's 64 positions (4 tiles)
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) acc[pt][0] = acc[pt][1] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u16x8 wf[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) wf[ct] = *(const u16x8*)(s3 + ((((wave * 2 + s) * 2 + ct) * 4 + g) * 16 + r16) * 8);
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) {
+        const int r = pt * 16 + r16;
+        const u16x8 pf = *(const u16x8*)(sa + (r * 8 + ((s * 4 + g) ^ (r & 7))) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[pt][ct] = T::mfma(wf[ct], pf, acc[pt][ct]);
+      }
+    }
+    // relu(conv3 + b3) + residual, relu -> 16-bit: to HBM and to the LDS tile
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const int r = pt * 16 + r16, m = m0 + r;
+      u16x4 q[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = relu(relu(acc[pt][ct][j] + bv3[ct][j]) + T::to_f32(rc[pt][4 * ct + j]));
+        q[ct] = T::pack4(v);
+      }
+      const u16x8 o = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      *(u16x8*)(sx + (r * 32 + ((4 * wave + g) ^ r16)) * 8) = o;
+      *(u16x8*)(m < M ? xo + (size_t)m * C3 + 32 * wave + 8 * g : g_sink + lane * 8) = o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // conv1: channel pairs (wave & 1) * PPW + pp, position tile pt2, K = 256
+    f32x4 acc1[PPW][2];
+#pragma unroll
+    for (int pp = 0; pp < PPW; ++pp) acc1[pp][0] = acc1[pp][1] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int r = pt2 * 16 + r16;
+      const u16x8 pf = *(const u16x8*)(sx + (r * 32 + ((s * 4 + g) ^ r16)) * 8);
+#pragma unroll
+      for (int pp = 0; pp < PPW; ++pp) {
+        const int P = (wave & 1) * PPW + pp;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const u16x8 wf = *(const u16x8*)(s1 + ((((P * 8 + s) * 2 + h) * 4 + g) * 16 + r16) * 8);
+          acc1[pp][h] = T::mfma(wf, pf, acc1[pp][h]);
+        }
+      }
+    }
+    const int m = m0 + pt2 * 16 + r16;
+    {
+#pragma unroll
+      for (int pp = 0; pp < PPW; ++pp) {
+        u16x4 q[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = relu(acc1[pp][h][j] + bv1[pp][h][j]);
+          q[h] = T::pack4(v);
+        }
+        *(u16x8*)(m < M ? ho + (size_t)m * N1 + 32 * ((wave & 1) * PPW + pp) + 8 * g : g_sink + lane * 8) =
+            __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+  }
+}
+
 // ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128, 256} — ResNet-50's
 // bottleneck expansions (conv3 64 -> 256 / 128 -> 512 + residual + ReLU,
 // ResVitKan.py:187's torchvision resnet50 layer1/layer2), their downsample
@@ -2319,6 +2475,45 @@ int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stre
   hipStream_t st = (hipStream_t)stream;
   if (d->dtype == FAC_DTYPE_BF16) convnd_pt<BF16, 128, false, true><<<G, 512, 0, st>>>(p, q);
   else convnd_pt<F16, 128, false, true><<<G, 512, 0, st>>>(p, q);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_bottleneck_pw2(const fac_conv_desc* c3, const fac_conv_desc* c1, void* stream) {
+  using namespace fac;
+  if (!c3 || !c1 || !c3->in || !c3->weight || !c3->bias || !c3->out || !c3->residual || !c1->weight || !c1->bias ||
+      !c1->out)
+    return FAC_ERR_ARG;
+  if (c3->dtype != c1->dtype || (c3->dtype != FAC_DTYPE_BF16 && c3->dtype != FAC_DTYPE_F16)) return FAC_ERR_ARG;
+  if (c3->flags != (FAC_CONV_RELU | FAC_CONV_RESID | FAC_CONV_RELU2) || c1->flags != FAC_CONV_RELU) return FAC_ERR_ARG;
+  auto pw = [](const fac_conv_desc* d) {
+    return d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 && d->pd == 0 &&
+           d->ph == 0 && d->pw == 0 && d->od == d->d && d->oh == d->h && d->ow == d->w && d->c_off == 0;
+  };
+  if (!pw(c3) || !pw(c1) || c3->cin != 64 || c3->cout != 256 || c3->k_pad != 64 || c3->ldo != 256 ||
+      c1->cin != 256 || c1->k_pad != 256 || (c1->cout != 64 && c1->cout != 128) || c1->ldo != c1->cout)
+    return FAC_ERR_SHAPE;
+  if (c1->n != c3->n || c1->d != c3->d || c1->h != c3->h || c1->w != c3->w) return FAC_ERR_SHAPE;
+  if (c3->ldr % 8 || c3->r_off % 8 || c3->ldr < c3->r_off + 256) return FAC_ERR_SHAPE;
+  const long long M = (long long)c3->n * c3->d * c3->h * c3->w;
+  if (M <= 0 || M >= (1LL << 31)) return FAC_ERR_SHAPE;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+    ncu = 256;
+  const int ntiles = (int)((M + 63) / 64), grid = std::min(ntiles, ncu);
+  hipStream_t st = (hipStream_t)stream;
+#define FAC_PW2(TT, N)                                                                                           \
+  bneck_pw2<TT, N><<<grid, 512, 0, st>>>((const uint16_t*)c3->in, (const uint16_t*)c3->weight, c3->bias,         \
+                                         (const uint16_t*)c3->residual, (const uint16_t*)c1->weight, c1->bias,   \
+                                         (uint16_t*)c3->out, (uint16_t*)c1->out, (int)M, c3->k_pad, c1->k_pad,   \
+                                         c3->ldr, c3->r_off)
+  if (c3->dtype == FAC_DTYPE_BF16) {
+    if (c1->cout == 64) FAC_PW2(BF16, 64);
+    else FAC_PW2(BF16, 128);
+  } else {
+    if (c1->cout == 64) FAC_PW2(F16, 64);
+    else FAC_PW2(F16, 128);
+  }
+#undef FAC_PW2
   return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 

@@ -273,6 +273,26 @@ def conv_dual(layer: ConvLayer, h: torch.Tensor, ds: ConvLayer, x: torch.Tensor,
     return out
 
 
+def bottleneck_pw2(c3: ConvLayer, h: torch.Tensor, res: torch.Tensor, c1: ConvLayer):
+    """(x, h1) = (relu(relu(c3(h)) + res), c1(x)) in one fac_bottleneck_pw2
+    launch: a ResNet-50 layer1 bottleneck's conv3 (+ bn3, identity residual)
+    and the next block's conv1 (+ bn1 + ReLU), the 256-channel block output
+    written once and not read back (ResVitKan.py:146-152).  Same values as
+    ``c3(h, residual=res, relu2=True)`` then ``c1(x)`` up to fp32 summation
+    order."""
+    n, d, hh, w, _ = h.shape
+    x = torch.empty(n, d, hh, w, c3.cout, device=h.device, dtype=h.dtype)
+    h1 = torch.empty(n, d, hh, w, c1.cout, device=h.device, dtype=h.dtype)
+    if tuple(res.shape) != tuple(x.shape) or res.dtype != h.dtype or not res.is_contiguous():
+        raise ValueError("bottleneck_pw2: residual must be the block input [N,D,H,W,256]")
+    d3 = _desc(c3, h, x, RELU | RESID | RELU2)
+    d3.residual, d3.ldr, d3.r_off = res.data_ptr(), res.shape[4], 0
+    d1 = _desc(c1, x, h1, RELU)
+    _lib.check(_lib.load().fac_bottleneck_pw2(ctypes.byref(d3), ctypes.byref(d1), _stream(h)), None,
+               "fac_bottleneck_pw2")
+    return x, h1
+
+
 def conv_split(layer: ConvLayer, x: torch.Tensor, splits, out0: torch.Tensor, c_off0: int, out1: torch.Tensor,
                out2: torch.Tensor, relu: bool = True) -> None:
     """One fac_conv_nd_split launch of `layer` (a conv over concatenated

@@ -35,8 +35,8 @@ from torch import nn
 
 from . import _lib
 from .cvit import MAX_SLOTS, _Node, reference_mask_poisons
-from .ops import (TORCH16, ConvLayer, KANLinearLayer, conv_dual, fold_bn, max_pool_sep, pack_input_s2d, pool, s2d_weight,
-                  sigmoid)
+from .ops import (TORCH16, ConvLayer, KANLinearLayer, bottleneck_pw2, conv_dual, fold_bn, max_pool_sep, pack_input_s2d,
+                  pool, s2d_weight, sigmoid)
 from .weights import kan_grid, resnet50_blocks, resvitkan_param_specs
 
 SUPPORTED = dict(image_size=224, patch_size=7, num_classes=2, channels=512, dim=1024, depth=6, heads=8,
@@ -192,6 +192,19 @@ class ResVitKan(nn.Module):
     # conv1 + bn1 + relu + maxpool as one launch (conv_s2d4_mp); FAC_RVK_MP=0:
     # conv_s2d4 then fac_pool_nd
     fuse_maxpool = os.environ.get("FAC_RVK_MP", "1") != "0"
+    # a layer1 bottleneck's conv3 and the next block's conv1 as one launch
+    # (fac_bottleneck_pw2); FAC_RVK_PW2=0: two launches
+    fuse_pw2 = os.environ.get("FAC_RVK_PW2", "1") != "0"
+
+    @staticmethod
+    def _pw2_ok(c3, c1n, x) -> bool:
+        """fac_bottleneck_pw2's shapes: conv3 1x1 64 -> 256, the next conv1 1x1
+        256 -> 64 / 128 at stride 1 (torchvision v1.5 puts the stride on conv2)."""
+        g3, g1 = c3.g, c1n.g
+        return (c3.cin == 64 and c3.cout == 256 and c1n.cin == 256 and c1n.cout in (64, 128)
+                and (g3.kd, g3.kh, g3.kw, g3.sd, g3.sh, g3.sw) == (1,) * 6
+                and (g1.kd, g1.kh, g1.kw, g1.sd, g1.sh, g1.sw) == (1,) * 6
+                and (g1.pd, g1.ph, g1.pw) == (0, 0, 0) and x.shape[-1] == 256)
 
     def _side_stream(self, device: torch.device):
         st = getattr(self, "_side", None)
@@ -219,11 +232,21 @@ class ResVitKan(nn.Module):
                 x = self._conv1(x16[b0:b0 + step])                  # 7x7/2 + bn1 + ReLU, on s2d cells
                 x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))  # MaxPool2d(3, 2, 1)
             tap(x)
-            for c1, c2, c3, ds in self._blocks:
+            h1 = None  # the next block's conv1 output, when the previous conv3 computed it
+            for bi, (c1, c2, c3, ds) in enumerate(self._blocks):
+                nxt = self._blocks[bi + 1] if bi + 1 < len(self._blocks) else None
+                if ds is None and self.fuse_pw2 and nxt is not None and self._pw2_ok(c3, nxt[0], x):
+                    # conv3 (+ identity residual) and the next block's conv1 in
+                    # one launch (fac_bottleneck_pw2): x is not read back
+                    x, h1n = bottleneck_pw2(c3, c2(h1 if h1 is not None else c1(x)), x, nxt[0])
+                    h1 = h1n
+                    tap(x)
+                    continue
                 if ds is not None and self.fuse_downsample:
                     # conv3 + bn3 + ReLU and the downsample conv + bn in one launch
                     # (fac_conv_nd_dual): the residual never goes through memory
-                    x = conv_dual(c3, c2(c1(x)), ds, x)
+                    x = conv_dual(c3, c2(h1 if h1 is not None else c1(x)), ds, x)
+                    h1 = None
                     tap(x)
                     continue
                 if ds is not None and self.side_downsample:
@@ -234,11 +257,12 @@ class ResVitKan(nn.Module):
                     side.wait_stream(main)
                     with torch.cuda.stream(side):
                         res = ds(x, relu=False)
-                    h = c2(c1(x))
+                    h = c2(h1 if h1 is not None else c1(x))
                     main.wait_stream(side)
                 else:
                     res = x if ds is None else ds(x, relu=False)
-                    h = c2(c1(x))
+                    h = c2(h1 if h1 is not None else c1(x))
+                h1 = None
                 x = c3(h, residual=res, relu2=True)                 # relu(bn3) + residual, relu
                 tap(x)
             self._channel(x, relu=False, out=out[b0:b0 + step])     # channel 1x1 + bn2

@@ -100,6 +100,18 @@ int fac_conv_nd_split(const fac_conv_desc* desc, void* out1, int ldo1, int split
  * Replaces fac_conv_nd(ds) + fac_conv_nd(desc with residual = its output). */
 int fac_conv_nd_dual(const fac_conv_desc* desc, const fac_conv_desc* ds, void* stream);
 
+/* A ResNet-50 layer1 bottleneck's conv3 and the next block's conv1 in one
+ * launch (ResVitKan.py:146-152; torchvision resnet50 layer1): c3 = the 1x1
+ * 64 -> 256 conv3 + bn3 with flags exactly FAC_CONV_RELU | FAC_CONV_RESID |
+ * FAC_CONV_RELU2 (out = relu(relu(conv + b) + residual), the block output,
+ * ldo 256); c1 = the next block's 1x1 256 -> 64 or 128 conv1 + bn1 with
+ * flags exactly FAC_CONV_RELU over the same positions: its input is c3's
+ * output (c1->in is ignored), written to c1->out (ldo = cout).  Every
+ * output is what fac_conv_nd(c3) then fac_conv_nd(c1) would produce up to
+ * fp32 summation order; the 256-channel map is written once and not read
+ * back.  FAC_ERR_ARG / FAC_ERR_SHAPE for anything else. */
+int fac_bottleneck_pw2(const fac_conv_desc* c3, const fac_conv_desc* c1, void* stream);
+
 /* Weight packing geometry for fac_conv_nd: *cout_pad = cout rounded up to
  * 128, *k_pad = taps*cin rounded up to 64. */
 int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad);

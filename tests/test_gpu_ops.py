@@ -95,6 +95,39 @@ def test_conv_nd_vs_torch_fp32(case, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("n1,hw", [(64, (56, 56)), (128, (23, 29))])
+def test_bottleneck_pw2_matches_two_launches(n1, hw, dt):
+    """fac_bottleneck_pw2 (a layer1 bottleneck's conv3 + identity residual and
+    the next block's conv1 in one launch) against the two separate
+    fac_conv_nd launches it replaces: the block output within one 16-bit ulp
+    on <= 5% of elements (fp32 summation order), the conv1 output within one
+    ulp of torch's fp32 conv of the fused kernel's own block output.  29x23
+    positions leave a partial last row tile."""
+    from fac_fake_amd.ops import ConvLayer, bottleneck_pw2
+    g = torch.Generator().manual_seed(5 + n1)
+    n = 3
+    h = torch.randn(n, 1, *hw, 64, generator=g).relu().to(T16[dt])
+    res = torch.randn(n, 1, *hw, 256, generator=g).relu().to(T16[dt])
+    w3, b3 = torch.randn(256, 64, 1, 1, 1, generator=g) / 8, torch.randn(256, generator=g) * 0.1
+    w1, b1 = torch.randn(n1, 256, 1, 1, 1, generator=g) / 16, torch.randn(n1, generator=g) * 0.1
+    c3 = ConvLayer(w3, b3, 1, 0, dtype=dt, device=DEV)
+    c1 = ConvLayer(w1, b1, 1, 0, dtype=dt, device=DEV)
+    hg, rg = h.to(DEV), res.to(DEV)
+    x, h1 = bottleneck_pw2(c3, hg, rg, c1)
+    xr = c3(hg, residual=rg, relu2=True)
+    h1r = c1(xr)
+    torch.cuda.synchronize()
+    u = _ulps(x.cpu(), xr.cpu(), dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05
+    if torch.equal(x.cpu(), xr.cpu()):
+        u1 = _ulps(h1.cpu(), h1r.cpu(), dt)
+        assert u1.max() <= 1.0 and (u1 > 0).float().mean() <= 0.05
+    ref1 = F.relu(F.conv3d(x.cpu().float().permute(0, 4, 1, 2, 3), w1.to(T16[dt]).float(), b1))
+    u2 = _ulps(h1.cpu(), ref1.permute(0, 2, 3, 4, 1).to(T16[dt]), dt)
+    assert u2.max() <= 1.0 and (u2 > 0).float().mean() <= 0.05
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("n,d,h,w", [(2, 1, 19, 59), (1, 2, 35, 31), (3, 1, 115, 115)])
 def test_conv_s2d4_maxpool_fused(n, d, h, w, dt):
     """conv_s2d4_mp (FAC_CONV_MAXPOOL3S2): the 4x4/1 space-to-depth conv +

@@ -107,6 +107,34 @@ def test_conv_maxpool_flag_argument_checks(built_lib):
     assert lib.fac_conv_nd(C.byref(desc(h=60)), None) == -1                        # 57 outputs: no 8 x 28 boxes
 
 
+def test_bottleneck_pw2_argument_checks(built_lib):
+    """fac_bottleneck_pw2 rejects null / mismatched descriptors before any
+    launch: FAC_ERR_ARG for pointers, dtypes and flags, FAC_ERR_SHAPE for
+    widths and positions."""
+    import ctypes as C
+    from fac_fake_amd import _lib
+    from fac_fake_amd.ops import ConvDesc, RELU, RELU2, RESID
+    lib = _lib.load()
+    assert lib.fac_bottleneck_pw2(None, None, None) == -1
+
+    def desc(cin, cout, flags, h=56):
+        d = ConvDesc()
+        d.dtype, d.inp, d.weight, d.bias, d.out, d.residual = 0, 16, 16, 16, 16, 16
+        d.n, d.d, d.h, d.w, d.cin, d.cout = 2, 1, h, h, cin, cout
+        d.kd = d.kh = d.kw = d.sd = d.sh = d.sw = 1
+        d.od, d.oh, d.ow = 1, h, h
+        d.k_pad = (cin + 63) // 64 * 64
+        d.ldo, d.ldr, d.flags = cout, 256, flags
+        return d
+
+    c3, c1 = desc(64, 256, RELU | RESID | RELU2), desc(256, 64, RELU)
+    assert lib.fac_bottleneck_pw2(C.byref(desc(64, 256, RELU | RESID)), C.byref(c1), None) == -1   # no RELU2
+    assert lib.fac_bottleneck_pw2(C.byref(c3), C.byref(desc(256, 64, 0)), None) == -1              # conv1 without ReLU
+    assert lib.fac_bottleneck_pw2(C.byref(desc(128, 256, RELU | RESID | RELU2)), C.byref(c1), None) == -2
+    assert lib.fac_bottleneck_pw2(C.byref(c3), C.byref(desc(256, 256, RELU)), None) == -2          # conv1 width
+    assert lib.fac_bottleneck_pw2(C.byref(c3), C.byref(desc(256, 64, RELU, h=28)), None) == -2     # positions differ
+
+
 def test_state_dict_is_the_reference_layout(golden):
     from fac_fake_amd.cvit import CViT
     want = list(golden("weights_checksums.json"))
