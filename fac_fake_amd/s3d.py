@@ -102,14 +102,19 @@ class S3D(nn.Module):
         sd = self.state_dict()
         dt = self.dtype_name
 
-        def bconv(p, stride=1, pad=0, cin_pad=None, kind="basic"):
+        def bconv(p, stride=1, pad=0, cin_pad=None, kind="basic", cout_pad=None):
             ck, bn = (f"{p}.conv", f"{p}.bn") if kind == "basic" else (f"{p}.conv_{kind}", f"{p}.bn_{kind}")
             w, b = fold_bn(sd[ck + ".weight"], None, sd[bn + ".weight"], sd[bn + ".bias"], sd[bn + ".running_mean"],
                            sd[bn + ".running_var"], BN_EPS)
+            if cout_pad:   # zero output channels (relu(0) = 0) up to cout_pad
+                w, b = _pad_rows(w, cout_pad), _pad_rows(b, cout_pad)
             return ConvLayer(w, b, stride, pad, dtype=dt, device=device, cin_pad=cin_pad)
 
-        def sep(p, k, s, pd, cin_pad=None):
-            return (bconv(p, (1, s, s), (0, pd, pd), cin_pad, "s"), bconv(p, (s, 1, 1), (pd, 0, 0), None, "t"))
+        def sep(p, k, s, pd, cin_pad=None, mid_pad=None):
+            # mid_pad: the (1,k,k) half's output (the (k,1,1) half's input)
+            # zero-padded to mid_pad channels
+            return (bconv(p, (1, s, s), (0, pd, pd), cin_pad, "s", cout_pad=mid_pad),
+                    bconv(p, (s, 1, 1), (pd, 0, 0), mid_pad, "t"))
 
         def sep_s2d(p):
             # base.0 without SRM: the (1,7,7)/(1,2,2) 3-channel conv as a (1,4,4)/1 conv over
@@ -150,6 +155,10 @@ class S3D(nn.Module):
                 # convs reading them take K steps that each lie in one tap
                 # (convnd_igemm's uniform-tap gather)
                 p1, p2 = self._pad64(b1a, 1), self._pad64(b2a, 2)
+                # and (FAC_S3D_PADT) the SepConvs' middle channels, so their
+                # (3,1,1) halves take the uniform-tap gather too
+                m1 = (b1b + 63) // 64 * 64 if self.padt else b1b
+                m2 = (b2b + 63) // 64 * 64 if self.padt else b2b
                 merged_p = merged
                 if (p1, p2) != (b1a, b2a):
                     hw = [heads[0][0], _pad_rows(heads[1][0], p1), _pad_rows(heads[2][0], p2)]
@@ -159,8 +168,8 @@ class S3D(nn.Module):
                 self._layers.append(("mixed", dict(
                     b0=bconv(f"{p}.branch0.0"), b1a=bconv(f"{p}.branch1.0"), b1=b1,
                     b2a=bconv(f"{p}.branch2.0"), b2=b2, b3=bconv(f"{p}.branch3.1"),
-                    b1p=b1 if p1 == b1a else sep(f"{p}.branch1.1", 3, 1, 1, cin_pad=p1),
-                    b2p=b2 if p2 == b2a else sep(f"{p}.branch2.1", 3, 1, 1, cin_pad=p2),
+                    b1p=b1 if (p1, m1) == (b1a, b1b) else sep(f"{p}.branch1.1", 3, 1, 1, cin_pad=p1, mid_pad=m1),
+                    b2p=b2 if (p2, m2) == (b2a, b2b) else sep(f"{p}.branch2.1", 3, 1, 1, cin_pad=p2, mid_pad=m2),
                     heads=merged, head_splits=(b0, b0 + b1a), head_widths=(b1a, b2a),
                     heads_p=merged_p, head_splits_p=(b0, b0 + p1), head_widths_p=(p1, p2),
                     widths=(b0, b1b, b2b, b3))))
@@ -181,6 +190,7 @@ class S3D(nn.Module):
     # channel padding of the merged heads' branch1.0 / branch2.0 outputs to a
     # multiple of 64: 0 none, 1 branch1.0 when >= 64 channels, 2 both
     pad64_level = int(os.environ.get("FAC_S3D_PAD64", "1"))
+    padt = os.environ.get("FAC_S3D_PADT", "1") == "1"
 
     def _pad64(self, c: int, level: int) -> int:
         if self.pad64_level < level or c % 64 == 0 or (level == 1 and c < 64):
