@@ -1230,6 +1230,116 @@ __global__ __launch_bounds__(512, 1) void bneck_pw2(const uint16_t* __restrict__
   }
 }
 
+// ---- bneck_pw2_l2: bneck_pw2 for ResNet-50 layer2 (conv3 1x1 128 -> 512 +
+// bn3 + ReLU + identity residual + ReLU, next conv1 1x1 512 -> 128 + bn1 +
+// ReLU).  The two weights (128 KB each) cannot both stay in LDS beside the
+// tiles, so each wave keeps its 64 conv3 output channels' weights in VGPRs
+// (16 fragments) and only the conv1 weight lives in LDS; tiles are 16 rows.
+// conv3 runs transposed with conv_pw's channel permutation (16-byte stores),
+// conv1 transposed over plain 16-channel tiles, one per wave (8-byte stores).
+template <class T>
+__global__ __launch_bounds__(512, 1) void bneck_pw2_l2(const uint16_t* __restrict__ a, const uint16_t* __restrict__ w3,
+                                                       const float* __restrict__ b3, const uint16_t* __restrict__ res,
+                                                       const uint16_t* __restrict__ w1, const float* __restrict__ b1,
+                                                       uint16_t* __restrict__ xo, uint16_t* __restrict__ ho, int M,
+                                                       int kp3, int kp1, int ldr, int r_off) {
+  constexpr int BM = 16, K3 = 128, C3 = 512, N1 = 128;
+  constexpr int W1EL = N1 * C3, AEL = BM * K3, XEL = BM * C3;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[W1EL + AEL + XEL];
+  uint16_t* const s1 = smem;
+  uint16_t* const sa = s1 + W1EL;  // A tile: rows of 16 pieces, piece p at p ^ row
+  uint16_t* const sx = sa + AEL;   // conv3 tile: rows of 64 pieces, piece q at q ^ row
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+
+  // conv3 weights of this wave's channels 64 wave + [0, 64) in registers:
+  // fragment (k-step s, tile ct), row i = channel 64 wave + 32 (ct >> 1) +
+  // 8 (i >> 2) + 4 (ct & 1) + (i & 3); lane (g, r16) holds row r16, k 32 s + 8 g
+  u16x8 wr[4][4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      const int n = 64 * wave + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
+      wr[s][ct] = *(const u16x8*)(w3 + (size_t)n * kp3 + 32 * s + 8 * g);
+    }
+  // conv1 weights in LDS, fragments [tile t][s][g][r16][8] (row i of tile t = channel 16 t + i)
+  for (int c = tid; c < N1 * (C3 / 8); c += 512) {
+    const int n = c >> 6, k8 = c & 63;
+    *(u16x8*)(s1 + ((((n >> 4) * 16 + (k8 >> 2)) * 4 + (k8 & 3)) * 16 + (n & 15)) * 8) =
+        *(const u16x8*)(w1 + (size_t)n * kp1 + k8 * 8);
+  }
+  float bv3[4][4], bv1[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv3[ct][j] = b3[64 * wave + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bv1[j] = b1[16 * wave + 4 * g + j];
+
+  const int ntiles = (M + BM - 1) / BM;
+  const int arow = tid >> 5, ah = tid & 31;  // this thread's 8-byte half-piece of a tile's A rows
+  u16x4 an;
+  u16x8 rn[2], rc[2];
+  auto load = [&](int t) {
+    const int m0 = t * BM;
+    an = *(const u16x4*)(a + (size_t)min(m0 + arow, M - 1) * K3 + ah * 4);
+    const int m = min(m0 + r16, M - 1);
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) rn[pp] = *(const u16x8*)(res + (size_t)m * ldr + r_off + 64 * wave + 32 * pp + 8 * g);
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  __syncthreads();  // conv1 weights in
+  for (; t < ntiles; t += gridDim.x) {
+    const int m0 = t * BM;
+    *(u16x4*)(sa + (arow * 16 + ((ah >> 1) ^ arow)) * 8 + (ah & 1) * 4) = an;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) rc[pp] = rn[pp];
+    if (t + (int)gridDim.x < ntiles) load(t + gridDim.x);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // conv3: this wave's 64 channels x the tile's 16 positions
+    f32x4 acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const u16x8 pf = *(const u16x8*)(sa + (r16 * 16 + ((s * 4 + g) ^ r16)) * 8);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) acc[ct] = T::mfma(wr[s][ct], pf, acc[ct]);
+    }
+    const int m = m0 + r16;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      u16x4 q[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[j] = relu(relu(acc[2 * pp + h][j] + bv3[2 * pp + h][j]) + T::to_f32(rc[pp][4 * h + j]));
+        q[h] = T::pack4(v);
+      }
+      const u16x8 o = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      *(u16x8*)(sx + (r16 * 64 + ((8 * wave + 4 * pp + g) ^ r16)) * 8) = o;
+      *(u16x8*)(m < M ? xo + (size_t)m * C3 + 64 * wave + 32 * pp + 8 * g : g_sink + lane * 8) = o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // conv1: channels 16 wave .. +15 x the 16 positions, K = 512
+    f32x4 acc1 = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const u16x8 pf = *(const u16x8*)(sx + (r16 * 64 + ((s * 4 + g) ^ r16)) * 8);
+      const u16x8 wf = *(const u16x8*)(s1 + (((wave * 16 + s) * 4 + g) * 16 + r16) * 8);
+      acc1 = T::mfma(wf, pf, acc1);
+    }
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = relu(acc1[j] + bv1[j]);
+    *(u16x4*)(m < M ? ho + (size_t)m * N1 + 16 * wave + 4 * g : g_sink + lane * 8) = T::pack4(v);
+  }
+}
+
 // ---- conv_pw: stride-1 1x1 convs with K = Cin in {64, 128, 256} — ResNet-50's
 // bottleneck expansions (conv3 64 -> 256 / 128 -> 512 + residual + ReLU,
 // ResVitKan.py:187's torchvision resnet50 layer1/layer2), their downsample
@@ -2489,18 +2599,34 @@ int fac_bottleneck_pw2(const fac_conv_desc* c3, const fac_conv_desc* c1, void* s
     return d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 && d->pd == 0 &&
            d->ph == 0 && d->pw == 0 && d->od == d->d && d->oh == d->h && d->ow == d->w && d->c_off == 0;
   };
-  if (!pw(c3) || !pw(c1) || c3->cin != 64 || c3->cout != 256 || c3->k_pad != 64 || c3->ldo != 256 ||
-      c1->cin != 256 || c1->k_pad != 256 || (c1->cout != 64 && c1->cout != 128) || c1->ldo != c1->cout)
-    return FAC_ERR_SHAPE;
+  const bool l1 = c3->cin == 64 && c3->cout == 256 && c3->k_pad == 64 && c1->cin == 256 && c1->k_pad == 256 &&
+                  (c1->cout == 64 || c1->cout == 128);
+  const bool l2 = c3->cin == 128 && c3->cout == 512 && c3->k_pad == 128 && c1->cin == 512 && c1->k_pad == 512 &&
+                  c1->cout == 128;
+  if (!pw(c3) || !pw(c1) || !(l1 || l2) || c3->ldo != c3->cout || c1->ldo != c1->cout) return FAC_ERR_SHAPE;
   if (c1->n != c3->n || c1->d != c3->d || c1->h != c3->h || c1->w != c3->w) return FAC_ERR_SHAPE;
-  if (c3->ldr % 8 || c3->r_off % 8 || c3->ldr < c3->r_off + 256) return FAC_ERR_SHAPE;
+  if (c3->ldr % 8 || c3->r_off % 8 || c3->ldr < c3->r_off + c3->cout) return FAC_ERR_SHAPE;
   const long long M = (long long)c3->n * c3->d * c3->h * c3->w;
   if (M <= 0 || M >= (1LL << 31)) return FAC_ERR_SHAPE;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
     ncu = 256;
-  const int ntiles = (int)((M + 63) / 64), grid = std::min(ntiles, ncu);
   hipStream_t st = (hipStream_t)stream;
+  if (l2) {
+    const int grid = (int)std::min<long long>((M + 15) / 16, ncu);
+    if (c3->dtype == FAC_DTYPE_BF16)
+      bneck_pw2_l2<BF16><<<grid, 512, 0, st>>>((const uint16_t*)c3->in, (const uint16_t*)c3->weight, c3->bias,
+                                               (const uint16_t*)c3->residual, (const uint16_t*)c1->weight, c1->bias,
+                                               (uint16_t*)c3->out, (uint16_t*)c1->out, (int)M, c3->k_pad, c1->k_pad,
+                                               c3->ldr, c3->r_off);
+    else
+      bneck_pw2_l2<F16><<<grid, 512, 0, st>>>((const uint16_t*)c3->in, (const uint16_t*)c3->weight, c3->bias,
+                                              (const uint16_t*)c3->residual, (const uint16_t*)c1->weight, c1->bias,
+                                              (uint16_t*)c3->out, (uint16_t*)c1->out, (int)M, c3->k_pad, c1->k_pad,
+                                              c3->ldr, c3->r_off);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  const int ntiles = (int)((M + 63) / 64), grid = std::min(ntiles, ncu);
 #define FAC_PW2(TT, N)                                                                                           \
   bneck_pw2<TT, N><<<grid, 512, 0, st>>>((const uint16_t*)c3->in, (const uint16_t*)c3->weight, c3->bias,         \
                                          (const uint16_t*)c3->residual, (const uint16_t*)c1->weight, c1->bias,   \

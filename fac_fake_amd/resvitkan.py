@@ -195,16 +195,20 @@ class ResVitKan(nn.Module):
     # a layer1 bottleneck's conv3 and the next block's conv1 as one launch
     # (fac_bottleneck_pw2); FAC_RVK_PW2=0: two launches
     fuse_pw2 = os.environ.get("FAC_RVK_PW2", "1") != "0"
+    # layer2's pairs too (bneck_pw2_l2): correct but measured slower than the
+    # two launches (69.3k vs 69.7-69.9k crops/s same box), so opt-in
+    fuse_pw2_l2 = os.environ.get("FAC_RVK_PW2_L2", "0") == "1"
 
     @staticmethod
     def _pw2_ok(c3, c1n, x) -> bool:
         """fac_bottleneck_pw2's shapes: conv3 1x1 64 -> 256, the next conv1 1x1
         256 -> 64 / 128 at stride 1 (torchvision v1.5 puts the stride on conv2)."""
         g3, g1 = c3.g, c1n.g
-        return (c3.cin == 64 and c3.cout == 256 and c1n.cin == 256 and c1n.cout in (64, 128)
-                and (g3.kd, g3.kh, g3.kw, g3.sd, g3.sh, g3.sw) == (1,) * 6
+        shapes = ((c3.cin == 64 and c3.cout == 256 and c1n.cin == 256 and c1n.cout in (64, 128))
+                  or (c3.cin == 128 and c3.cout == 512 and c1n.cin == 512 and c1n.cout == 128 and ResVitKan.fuse_pw2_l2))
+        return (shapes and (g3.kd, g3.kh, g3.kw, g3.sd, g3.sh, g3.sw) == (1,) * 6
                 and (g1.kd, g1.kh, g1.kw, g1.sd, g1.sh, g1.sw) == (1,) * 6
-                and (g1.pd, g1.ph, g1.pw) == (0, 0, 0) and x.shape[-1] == 256)
+                and (g1.pd, g1.ph, g1.pw) == (0, 0, 0) and x.shape[-1] == c3.cout)
 
     def _side_stream(self, device: torch.device):
         st = getattr(self, "_side", None)

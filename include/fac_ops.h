@@ -100,11 +100,12 @@ int fac_conv_nd_split(const fac_conv_desc* desc, void* out1, int ldo1, int split
  * Replaces fac_conv_nd(ds) + fac_conv_nd(desc with residual = its output). */
 int fac_conv_nd_dual(const fac_conv_desc* desc, const fac_conv_desc* ds, void* stream);
 
-/* A ResNet-50 layer1 bottleneck's conv3 and the next block's conv1 in one
- * launch (ResVitKan.py:146-152; torchvision resnet50 layer1): c3 = the 1x1
- * 64 -> 256 conv3 + bn3 with flags exactly FAC_CONV_RELU | FAC_CONV_RESID |
- * FAC_CONV_RELU2 (out = relu(relu(conv + b) + residual), the block output,
- * ldo 256); c1 = the next block's 1x1 256 -> 64 or 128 conv1 + bn1 with
+/* A ResNet-50 layer1 / layer2 bottleneck's conv3 and the next block's conv1
+ * in one launch (ResVitKan.py:146-152; torchvision resnet50): c3 = the 1x1
+ * 64 -> 256 (layer1) or 128 -> 512 (layer2) conv3 + bn3 with flags exactly
+ * FAC_CONV_RELU | FAC_CONV_RESID | FAC_CONV_RELU2 (out = relu(relu(conv + b)
+ * + residual), the block output, ldo = cout); c1 = the next block's 1x1
+ * 256 -> 64 / 128 (layer1) or 512 -> 128 (layer2) conv1 + bn1 with
  * flags exactly FAC_CONV_RELU over the same positions: its input is c3's
  * output (c1->in is ignored), written to c1->out (ldo = cout).  Every
  * output is what fac_conv_nd(c3) then fac_conv_nd(c1) would produce up to

@@ -95,21 +95,24 @@ def test_conv_nd_vs_torch_fp32(case, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
-@pytest.mark.parametrize("n1,hw", [(64, (56, 56)), (128, (23, 29))])
-def test_bottleneck_pw2_matches_two_launches(n1, hw, dt):
+@pytest.mark.parametrize("cin,cmid,n1,hw", [(64, 256, 64, (56, 56)), (64, 256, 128, (23, 29)),
+                                            (128, 512, 128, (28, 28)), (128, 512, 128, (13, 11))])
+def test_bottleneck_pw2_matches_two_launches(cin, cmid, n1, hw, dt):
     """fac_bottleneck_pw2 (a layer1 bottleneck's conv3 + identity residual and
     the next block's conv1 in one launch) against the two separate
     fac_conv_nd launches it replaces: the block output within one 16-bit ulp
     on <= 5% of elements (fp32 summation order), the conv1 output within one
-    ulp of torch's fp32 conv of the fused kernel's own block output.  29x23
-    positions leave a partial last row tile."""
+    ulp of torch's fp32 conv of the fused kernel's own block output.  Layer1
+    (64 -> 256 -> 64 / 128, bneck_pw2) and layer2 (128 -> 512 -> 128,
+    bneck_pw2_l2) shapes; 29x23 and 13x11 positions leave a partial last row
+    tile."""
     from fac_fake_amd.ops import ConvLayer, bottleneck_pw2
     g = torch.Generator().manual_seed(5 + n1)
     n = 3
-    h = torch.randn(n, 1, *hw, 64, generator=g).relu().to(T16[dt])
-    res = torch.randn(n, 1, *hw, 256, generator=g).relu().to(T16[dt])
-    w3, b3 = torch.randn(256, 64, 1, 1, 1, generator=g) / 8, torch.randn(256, generator=g) * 0.1
-    w1, b1 = torch.randn(n1, 256, 1, 1, 1, generator=g) / 16, torch.randn(n1, generator=g) * 0.1
+    h = torch.randn(n, 1, *hw, cin, generator=g).relu().to(T16[dt])
+    res = torch.randn(n, 1, *hw, cmid, generator=g).relu().to(T16[dt])
+    w3, b3 = torch.randn(cmid, cin, 1, 1, 1, generator=g) / np.sqrt(cin), torch.randn(cmid, generator=g) * 0.1
+    w1, b1 = torch.randn(n1, cmid, 1, 1, 1, generator=g) / np.sqrt(cmid), torch.randn(n1, generator=g) * 0.1
     c3 = ConvLayer(w3, b3, 1, 0, dtype=dt, device=DEV)
     c1 = ConvLayer(w1, b1, 1, 0, dtype=dt, device=DEV)
     hg, rg = h.to(DEV), res.to(DEV)
