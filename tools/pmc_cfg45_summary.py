@@ -7,7 +7,9 @@ the dispatch count, mean counters per dispatch, MFMA busy fraction, LDS and
 wave-state ratios and HBM bytes per dispatch (2 x FETCH_SIZE + WRITE_SIZE,
 KiB, the gfx950 correction of tools/rocprof_summary.py); and for the whole
 eager forward the cycle-weighted MFMA busy fraction (sum of MFMA busy cycles
-over sum of 1024 x GRBM_GUI_ACTIVE / 8) and the HBM bytes per forward.
+over sum of 1024 x GRBM_GUI_ACTIVE / 8) and the HBM bytes per forward, over
+the fac:: kernels only (the runtime's copyBuffer dispatches are the one-time
+weight uploads of the first forward).
 """
 import csv
 import json
@@ -41,7 +43,8 @@ def summarise(src: Path, model: str, forwards: int) -> dict:
         for p in passes:
             for c, v in p.get(k, {}).items():
                 vals[c] = sum(v) / len(v)
-                tot[c] += sum(v)
+                if k.startswith("fac::"):  # runtime copies / torch fills: one-time setup, not the forward
+                    tot[c] += sum(v)
                 n = max(n, len(v))
         m = {"dispatches": n, **{c: round(v, 1) for c, v in vals.items()}, **derive(vals)}
         if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
