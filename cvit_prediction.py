@@ -41,7 +41,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 
 from fac_fake_amd.prediction import (label, non_empty, pre_process_prediction, pred_sig,  # noqa: E402,F401
                                      pred_tensor)
-from fac_fake_amd.video import MAX_CROPS_REFERENCE, crop_faces, predict_video  # noqa: E402
+from fac_fake_amd.video import (MAX_CROPS_REFERENCE, crop_faces, predict_video, score_selected,  # noqa: E402
+                                select_reference)
 
 mean = [0.485, 0.456, 0.406]    # cvit_prediction.py:41 (fused into conv1 here)
 std = [0.229, 0.224, 0.225]     # cvit_prediction.py:42
@@ -113,17 +114,35 @@ def predict(filename, mtcnn=None, mode: str = "reference"):
     return predict_video(model, fr, boxes, mode=mode)
 
 
-def predict_on_video(dfdc_filenames, num_workers):
-    """Scores of the videos ``sample/<filename>`` in order (:73-83): a
-    ``ThreadPoolExecutor(num_workers)`` map over ``predict``, like the
-    reference (which runs it with one worker, :303)."""
-    def process_file(i):
-        filename = dfdc_filenames[i]
-        return predict(os.path.join(sample, filename), None)
+def predict_on_video(dfdc_filenames, num_workers, batch: int = 256):
+    """Scores of the videos ``sample/<filename>`` in order (:73-83).
 
-    with ThreadPoolExecutor(max_workers=num_workers) as ex:
-        predictions = ex.map(process_file, range(len(dfdc_filenames)))
-    return list(predictions)
+    The reference maps ``predict`` over a ``ThreadPoolExecutor(num_workers)``
+    (one worker, :303), i.e. one <= 29-crop forward per video.  Here the
+    ``num_workers`` threads only read the files and keep each video's crop
+    selection and the frames it needs (``select_reference``); the GPU work
+    stays on the calling thread, which scores the crops of consecutive videos
+    together in forwards of up to ``batch`` crops (``score_selected``: each
+    video keeps its own slots 0..n-1, one segmented score launch per group).
+    Every score is bit-identical to ``predict`` on that video alone."""
+    if model is None:
+        raise RuntimeError("call load_model() first (the reference builds its model at import)")
+
+    def load(i):
+        frames, boxes = read_video(os.path.join(sample, dfdc_filenames[i]))
+        return select_reference(frames, boxes)
+
+    predictions, group, ncrops = [], [], 0
+    with ThreadPoolExecutor(max_workers=max(1, int(num_workers))) as ex:
+        for item in ex.map(load, range(len(dfdc_filenames))):
+            if group and ncrops + len(item[1]) > batch:
+                predictions += score_selected(model, group, batch)
+                group, ncrops = [], 0
+            group.append(item)
+            ncrops += len(item[1])
+        if group:
+            predictions += score_selected(model, group, batch)
+    return predictions
 
 
 def real_or_fake(filenames, predictions):

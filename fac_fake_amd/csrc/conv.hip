@@ -390,6 +390,204 @@ __global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_
   store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
 }
 
+// ---------------------------------------------------------------------------
+// conv3x3_db: the same implicit GEMM with the weight (B) fragments loaded
+// straight from global memory (L2) into VGPRs instead of through an LDS ring.
+//
+// Why: in conv3x3_bn_relu every tap step streams a [BN][32] weight slice into
+// LDS with global_load_lds and then needs a workgroup barrier before any wave
+// may read it, although with a 1 x WN wave grid each wave reads only its own
+// BN/WN columns: the slice is not shared at all.  Round 1 measured the deep
+// layers 20-27 % faster without that glds and 4 % without the per-tap barrier
+// (DESIGN §3.4).  Here each wave fetches its CTW B fragments (16 columns x 32
+// k each = one 16-byte load per lane) two tap steps ahead with
+// global_load_dwordx4, so the only LDS traffic left is the shared halo (A)
+// and the only barrier is one per 32-channel chunk (halo double buffer).
+//
+// No LDS-DMA at all: the next chunk's halo is fetched at tap 0 with plain
+// 16-byte loads into registers and written to the other halo buffer after
+// tap 1.  Every vector-memory op of the loop is then a plain load, and the
+// compiler's own `s_waitcnt vmcnt` (before the MFMAs and ds_writes that use
+// them) is exact: LLVM counts LDS-DMA and loads as different event types
+// and, with both pending, falls back to vmcnt(0).  (An async load must never
+// be an inline-asm output either: the compiler takes such a value as written
+// at the asm and may reuse its registers -- a dummy load's, once dead --
+// before the data lands; a first version faulted that way.)
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restrict__ in,
+                                                       const uint16_t* __restrict__ wpk,
+                                                       const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                       int H, int W, int Cin, int Cout,
+                                                       const uint16_t* __restrict__ zero16, int do_relu) {
+  constexpr int CK = CONV_CK;
+  constexpr int HH = TH + 2, HWD = TW + 2;
+  constexpr int NPIX = TH * TW;
+  constexpr int RT = ((NPIX + 15) / 16 + WM - 1) / WM * WM;
+  constexpr int RTW = RT / WM;
+  constexpr int CTW = BN / 16 / WN;
+  constexpr int RPX = TW == 14 ? HWD + 1 : HWD;  // pixel-major halo row pitch (as conv3x3_bn_relu's PM image)
+  constexpr int HSLOTS = (HH * RPX * 4 + 255) / 256 * 256;
+  constexpr int HPW = HSLOTS / 256;
+  constexpr int HALO = HSLOTS * 8;
+  constexpr int WSL = BN * CK;
+  constexpr int OPS = BN + 8;
+  constexpr int OPER = 2 * HALO;
+  constexpr int OSTG = (POOL ? RT * 4 : RT * 16) * OPS;
+  constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(TH % 2 == 0 && TW % 2 == 0, "window-major order needs even boxes");
+  static_assert(CTW * 16 * WN == BN, "BN split");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
+  int bx = blockIdx.x;  // XCD-aware box order (conv3x3_bn_relu)
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  const int b = bx / tiles_per_img;
+  const int tile = bx - b * tiles_per_img;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int nb = blockIdx.y;
+  const int nchunks = Cin / CK;
+  const int nsteps = nchunks * 9;
+  const uint16_t* in_b = in + (size_t)b * H * W * Cin;
+  const uint16_t* wsrc = wpk + (size_t)nb * nchunks * 9 * WSL;
+
+  // Halo map: slot (i*4 + wave)*64 + lane of the pixel-major image holds 16
+  // bytes of pixel (hy, hx), channel piece q; out-of-image and pitch-padding
+  // slots read the zero page (every lane loads, so the loads stay uniform).
+  int hsrc[HPW];
+#pragma unroll
+  for (int i = 0; i < HPW; ++i) {
+    const int slot = (i * 4 + wave) * 64 + lane;
+    const int pix = slot >> 2;
+    const int hy = pix / RPX, hx = pix - (pix / RPX) * RPX;
+    const int q = hy < HH ? (slot & 3) ^ ((hy & 1) << 1) : 4;
+    const int y = y0 + hy - 1, x = x0 + hx - 1;
+    hsrc[i] = -1;
+    if (q < 4 && hx < HWD && y >= 0 && y < H && x >= 0 && x < W) hsrc[i] = (y * W + x) * Cin + q * 8;
+  }
+  u16x8 hreg[HPW];
+  auto load_halo = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) {
+      const uint16_t* src = hsrc[i] >= 0 ? in_b + hsrc[i] + c * CK : zero16;
+      hreg[i] = *(const u16x8*)src;
+    }
+  };
+  auto store_halo = [&](uint16_t* dst) {
+#pragma unroll
+    for (int i = 0; i < HPW; ++i) *(u16x8*)(dst + ((i * 4 + wave) * 64 + lane) * 8) = hreg[i];
+  };
+  // B fragment of column tile ct: lane (n = lane & 15, k piece lane >> 4)
+  // reads 16 bytes at ((kq * BN + wn * CTW * 16 + ct * 16 + n) * 8) of the slice
+  const int boff = ((lane >> 4) * BN + wn * CTW * 16 + (lane & 15)) * 8;
+  auto load_b = [&](u16x8(&dst)[CTW], int s) {
+    const uint16_t* sb = wsrc + (size_t)(s < nsteps ? s : 0) * WSL + boff;  // past the end: a dummy re-read
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) dst[ct] = *(const u16x8*)(sb + ct * 128);
+  };
+
+  int abase[RTW];
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt) {
+    int m = (wm * RTW + rt) * 16 + (lane & 15);
+    if (m >= NPIX) m = 0;
+    int py, px;
+    box_pixel<TW>(m, py, px);
+    abase[rt] = ((py * RPX + px) * 4 + ((lane >> 4) ^ ((py & 1) << 1))) * 8;
+  }
+
+  f32x4 acc[RTW][CTW];
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = (f32x4)0.f;
+
+  u16x8 bq[3][CTW];
+  load_halo(0);
+  load_b(bq[0], 0);
+  load_b(bq[1], 1);
+  store_halo(smem);
+  __syncthreads();
+  u16x8 fa[RTW];
+#pragma unroll
+  for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(smem + abase[rt]);
+
+  // Step s = 9c + t: at its top B(s+2) is fetched into slot (t+2) % 3 and (t
+  // = 0) the next chunk's halo into registers; after tap 1 those registers go
+  // to the other halo buffer.  Tap t multiplies fragments read during tap t-1
+  // and reads tap t+1's behind each row tile's MFMAs.  The end of t = 7 is
+  // the chunk's only barrier: after it tap 0 of the next chunk can be read (t
+  // = 8), and every wave is past its last read of the buffer the chunk after
+  // next overwrites (at its t = 1).
+  for (int c = 0; c < nchunks; ++c) {
+    const uint16_t* hb = smem + (c & 1) * HALO;
+    uint16_t* hbn = smem + ((c + 1) & 1) * HALO;
+    const int s0 = c * 9;
+    auto step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      load_b(bq[(t + 2) % 3], s0 + t + 2);
+      if constexpr (t == 0) load_halo(c + 1 < nchunks ? c + 1 : c);
+      constexpr int kyn = t < 8 ? (t + 1) / 3 : 0, kxn = t < 8 ? (t + 1) % 3 : 0;
+      constexpr int ntoff = (kyn * RPX + kxn) * 32;
+      const uint16_t* hnx = t < 8 ? hb : hbn;
+#pragma unroll
+      for (int rt = 0; rt < RTW; ++rt) {
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bq[t % 3][ct], acc[rt][ct]);
+        fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, CTW + (t == 0 ? HPW : 0), 0);
+#pragma unroll
+      for (int rt = 0; rt < RTW; ++rt) {
+        __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      if constexpr (t == 1) store_halo(hbn);
+      if constexpr (t == 7) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{});
+    step(std::integral_constant<int, 7>{});
+    step(std::integral_constant<int, 8>{});
+  }
+  __syncthreads();
+
+  uint16_t* ostg = smem;
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int nl = (wn * CTW + ct) * 16 + (lane & 15);
+    const float bv = bias[nb * BN + nl];
+#pragma unroll
+    for (int rt = 0; rt < RTW; ++rt) {
+      const f32x4 v = acc[rt][ct];
+      if constexpr (POOL) {
+        const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        const int w = (wm * RTW + rt) * 4 + (lane >> 4);
+        ostg[w * OPS + nl] = T::from_f32(do_relu ? relu(mx + bv) : mx + bv);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int m = (wm * RTW + rt) * 16 + (lane >> 4) * 4 + j;
+          ostg[m * OPS + nl] = T::from_f32(do_relu ? relu(v[j] + bv) : v[j] + bv);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
+  const int oy0 = POOL ? y0 / 2 : y0, ox0 = POOL ? x0 / 2 : x0;
+  store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
+}
+
 // conv1 (3 -> 32 @224) with the input normalisation of cvit_prediction.py:
 // x/255 then (x - mean_c)/std_c (:41-42, :214-215), zero padding applied in
 // normalised space exactly like the reference's Conv2d(padding=1).
@@ -546,58 +744,56 @@ static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const floa
   return hipSuccess;
 }
 
-// FAC_CONV_NBOX=2: the 56 / 28 tiles as 8-wave two-box workgroups
-static int conv_nbox() {
-  static const int n = [] {
-    const char* e = std::getenv("FAC_CONV_NBOX");
-    return e && e[0] == '2' ? 2 : 1;
-  }();
-  return n;
+// conv3x3_db launch (weights straight to VGPRs, one barrier per chunk)
+template <class T, int TH, int TW, int BN, int WM, int WN, int OCC = 2>
+static hipError_t launch_db(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
+                            int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
+  dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
+  if (pool)
+    conv3x3_db<T, TH, TW, BN, WM, WN, true, OCC><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  else
+    conv3x3_db<T, TH, TW, BN, WM, WN, false, OCC><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  return hipSuccess;
 }
 
-// FAC_CONV_POOL112_OCC=4: the pooled 112^2 tile (conv6) at 4 workgroups per CU, as conv4/5
-static int conv_pool112_occ() {
-  static const int n = [] {
-    const char* e = std::getenv("FAC_CONV_POOL112_OCC");
-    return e ? std::atoi(e) : 2;
-  }();
-  return n;
-}
+static int g_conv_db = 0;  // A/B switch (fac_set_option "conv_db"), bit k: resolution 56 / 28 / 14
+void set_conv_db(int v) { g_conv_db = v; }
 
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                                 int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st,
                                 int relu) {
   if (W != H) return hipErrorInvalidValue;
+  if (g_conv_db) {
+    switch (H * 1000 + conv_block_n(H, Cout)) {
+      case 56128:
+        if (g_conv_db & 1) return launch_db<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+        break;
+      case 28256:
+        if (g_conv_db & 2) return launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+        break;
+      case 14128:
+        if (g_conv_db & 8) return launch_db<T, 14, 14, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+        if (g_conv_db & 4) return launch_db<T, 14, 14, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+        break;
+      default: break;
+    }
+  }
   switch (H * 1000 + conv_block_n(H, Cout)) {
     case 224032: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
     // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
     case 112064:
       // the pooled tile (conv6) spills at 4 per CU (128 VGPRs): 2 per CU
-      // (same box: conv4-6 0.665 -> 0.60 ms; FAC_CONV_POOL112_OCC=4 restores)
-      if (pool && conv_pool112_occ() != 4)
+      // (same box: conv4-6 0.665 -> 0.60 ms)
+      if (pool)
         launch_box<T, 16, 16, 64, 4, 1, 1, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       else
         launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       break;
-    case 56128:
-      if (conv_nbox() == 2 && (B * 14) % 2 == 0) {
-        if (launch_box<T, 8, 28, 128, 2, 2, 2, 1, true, true, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
-          return hipErrorInvalidValue;
-      } else {
-        launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      }
-      break;
+    case 56128: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 56064: launch_box<T, 8, 28, 64, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 28256:
-      if (conv_nbox() == 2 && (B * 7) % 2 == 0) {
-        if (launch_box<T, 4, 28, 256, 1, 4, 2, 1, true, true, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
-          return hipErrorInvalidValue;
-      } else {
-        launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      }
-      break;
+    case 28256: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28192: launch_box<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28128: launch_box<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // (a two-box 14x14 workgroup needs 256+ VGPRs and spills: not built)

@@ -22,6 +22,7 @@
 
 namespace fac {
 int conv_block_n(int H, int cout);
+void set_conv_db(int v);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
@@ -44,6 +45,7 @@ hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, fl
 hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, float* logits, float* probs, int B,
                            hipStream_t st);
 hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st);
+hipError_t launch_video_score_seg(const float* logits, const int* seg, int nv, float* score, hipStream_t st);
 hipError_t launch_crop_resize(const uint8_t* frames, int n_frames, int H, int W, const int32_t* boxes, int n_boxes,
                               uint8_t* crops, hipStream_t st);
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
@@ -720,6 +722,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     c->stem_ev_used = 0;
     return FAC_OK;
   }
+  if (k == "conv_db") {  // A/B: conv3x3_db for the 56 / 28 / 14 tiles (bits 1 / 2 / 4), process-wide
+    fac::set_conv_db(value);
+    return FAC_OK;
+  }
   if (k == "stem_dynamic") {
     c->stem_dynamic = value != 0;
     return FAC_OK;
@@ -914,6 +920,13 @@ int fac_check_device_errors(fac_ctx* c, int* flags) {
 int fac_video_score(const float* d_logits, int n, float* d_score, void* stream) {
   if (!d_score || n < 0 || (n > 0 && !d_logits)) return FAC_ERR_ARG;
   return fac::launch_video_score(d_logits, n, d_score, (hipStream_t)stream) == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_video_score_seg(const float* d_logits, const int* d_seg, int nv, float* d_scores, void* stream) {
+  if (nv < 0 || (nv > 0 && (!d_logits || !d_seg || !d_scores))) return FAC_ERR_ARG;
+  if (nv == 0) return FAC_OK;
+  return fac::launch_video_score_seg(d_logits, d_seg, nv, d_scores, (hipStream_t)stream) == hipSuccess ? FAC_OK
+                                                                                                   : FAC_ERR_HIP;
 }
 
 const char* fac_last_error(fac_ctx* c) { return c ? c->err.c_str() : "null context"; }

@@ -2132,13 +2132,9 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
 }
 
 // grid of gx row tiles x ny column tiles: flat (column tiles of a row tile
-// adjacent, see convnd_igemm) unless FAC_CONV_FLAT=0 or it would overflow
+// adjacent, see convnd_igemm) unless it would overflow
 static dim3 conv_grid(ConvP& p, int gx, int ny) {
-  static const bool flat = [] {
-    const char* e = std::getenv("FAC_CONV_FLAT");
-    return !(e && e[0] == '0');
-  }();
-  if (flat && ny > 1 && (long long)gx * ny < INT_MAX) {
+  if (ny > 1 && (long long)gx * ny < INT_MAX) {
     p.ny = ny;
     return dim3(gx * ny, 1);
   }
@@ -2148,12 +2144,8 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
 
 template <class T>
 static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
-  static const int pt_mode = [] {
-    const char* e = std::getenv("FAC_ND_PT");  // 0 off, 128 / 256 force the tile width
-    return e ? std::atoi(e) : 1;
-  }();
   const bool res = p.flags & FAC_CONV_RESID;
-  if (!pt_mode || p.Cout % 128 || p.ksteps < 2 || !p.vec_out || p.split1 < p.Cout ||
+  if (p.Cout % 128 || p.ksteps < 2 || !p.vec_out || p.split1 < p.Cout ||
       (p.flags & FAC_CONV_OUT_F32) || (!res && (p.flags & FAC_CONV_RELU2)) || (res && !p.vec_res))
     return false;
   static const int ncu = [] {
@@ -2163,7 +2155,7 @@ static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
     return n;
   }();
   const int nrt = (p.M + 255) / 256;
-  const int bn = res ? 128 : (pt_mode == 128 || pt_mode == 256 ? pt_mode : (p.Cout % 256 == 0 ? 256 : 128));
+  const int bn = res ? 128 : (p.Cout % 256 == 0 ? 256 : 128);
   if (p.Cout % bn) return false;
   const int ny = p.Cout / bn;
   int G = ncu / ny * ny;
@@ -2183,32 +2175,7 @@ static void launch_convnd_t(ConvP p, hipStream_t st) {
   }
   const int gx64 = (p.M + 63) / 64, gx128 = (p.M + 127) / 128, gx256 = (p.M + 255) / 256;
   const int ny64 = (p.Cout + 63) / 64, ny128 = (p.Cout + 127) / 128;
-  // FAC_ND_TILE forces one tile (layer A/Bs: tools/nd_layers.py): 1 = 128x64
-  // (2/CU), 2 = 256x128, 3 = 128x64 2-slot (3/CU), 4 = 64x64
-  static const int force = [] {
-    const char* e = std::getenv("FAC_ND_TILE");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (force == 1 || (force == 2 && p.Cout % 128)) {
-    convnd_igemm<T, 128, 64, 2, 2, 2, 3, UT, IL><<<conv_grid(p, gx128, ny64), 256, 0, st>>>(p);
-    return;
-  }
-  if (force == 2) {
-    convnd_igemm<T, 256, 128, 4, 2, 1, 3, UT, IL><<<conv_grid(p, gx256, ny128), 512, 0, st>>>(p);
-    return;
-  }
-  if (force == 3) {
-    convnd_igemm<T, 128, 64, 2, 2, 3, 2, UT, IL><<<conv_grid(p, gx128, ny64), 256, 0, st>>>(p);
-    return;
-  }
-  if (force == 4) {
-    convnd_igemm<T, 64, 64, 2, 2, 3, 3, UT, IL><<<conv_grid(p, gx64, ny64), 256, 0, st>>>(p);
-    return;
-  }
-  static const int nd256_min = [] {
-    const char* e = std::getenv("FAC_ND256_MIN");
-    return e ? std::atoi(e) : 256;
-  }();
+  constexpr int nd256_min = 256;  // 256 x 128 tiles only when they fill the chip at least once
   if (p.ksteps <= 2) {
     // K <= 128 (1x1 expansions): memory-bound, so occupancy first — a 2-slot
     // ring (48 KB) lets three 128 x 64 workgroups share a CU
@@ -2222,7 +2189,7 @@ static void launch_convnd_t(ConvP p, hipStream_t st) {
     // 256 x 128 tiles (8 waves, 144 KB ring, one per CU: 48 KB global -> LDS per
     // 4.2 MFLOP, twice the 128 x 64 tile's intensity) when the grid still fills
     // the chip at least once (ResNet's 7x7 layers: 392 tiles, 1.2-1.35x faster
-    // than 128 x 64 ones; FAC_ND256_MIN, same-box config 5 +2 %) and no column
+    // than 128 x 64 ones; same-box config 5 +2 %) and no column
     // tile is half empty
     const dim3 g = conv_grid(p, gx256, ny128);
     convnd_igemm<T, 256, 128, 4, 2, 1, 3, UT, IL><<<g, 512, 0, st>>>(p);
@@ -2235,25 +2202,10 @@ static void launch_convnd_t(ConvP p, hipStream_t st) {
 template <class T>
 static hipError_t launch_convnd(ConvP p, int cout_pad, hipStream_t st) {
   (void)cout_pad;
-  static const bool ut_on = [] {
-    const char* e = std::getenv("FAC_CONV_UT");
-    return !(e && e[0] == '0');
-  }();
-  static const bool il_on = [] {
-    const char* e = std::getenv("FAC_ND_IL");
-    return !(e && e[0] == '0');
-  }();
-  static const bool il_g = [] {
-    const char* e = std::getenv("FAC_ND_IL_G");  // interleaved issue on the general (per-lane tap) gather too
-    return !(e && e[0] == '0');
-  }();
-  if (ut_on && p.C8 % 8 == 0) {
-    if (il_on) launch_convnd_t<T, true, true>(p, st);
-    else launch_convnd_t<T, true, false>(p, st);
-  } else {
-    if (il_on && il_g) launch_convnd_t<T, false, true>(p, st);
-    else launch_convnd_t<T, false, false>(p, st);
-  }
+  // uniform-tap gather when every 64-deep K step lies in one tap (cin % 64),
+  // the per-lane tap gather otherwise; both with the interleaved glds issue
+  if (p.C8 % 8 == 0) launch_convnd_t<T, true, true>(p, st);
+  else launch_convnd_t<T, false, true>(p, st);
   return hipGetLastError();
 }
 
@@ -2369,23 +2321,11 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   // stride-1 1x1 convs with K = cin in {64, 128, 256}: conv_pw
-  static const bool pw_on = [] {
-    const char* e = std::getenv("FAC_CONV_PW");
-    return !(e && e[0] == '0');
-  }();
-  static const bool pw256 = [] {
-    const char* e = std::getenv("FAC_PW_K256");
-    return !(e && e[0] == '0');
-  }();
-  static const bool pw_pt = [] {
-    // K 128 / 256 1x1s with cout % 128 == 0 go to convnd_pt (FAC_PW_PT=0: conv_pw):
-    // config 5 +1.2 % same-box (layer3's 256 -> 1024 + residual 160 -> 145 us)
-    const char* e = std::getenv("FAC_PW_PT");
-    return !(e && e[0] == '0');
-  }();
-  const bool to_pt = pw_pt && (d->cin == 128 || d->cin == 256) && d->cout % 128 == 0;
-  if (pw_on && !split && !to_pt && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
-      d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->cin == 64 || d->cin == 128 || (d->cin == 256 && pw256)) &&
+  // K 128 / 256 1x1s with cout % 128 == 0 go to convnd_pt instead: config 5
+  // +1.2 % same-box (layer3's 256 -> 1024 + residual 160 -> 145 us)
+  const bool to_pt = (d->cin == 128 || d->cin == 256) && d->cout % 128 == 0;
+  if (!split && !to_pt && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+      d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->cin == 64 || d->cin == 128 || d->cin == 256) &&
       k_pad == d->cin &&
       d->cout % 64 == 0 && d->ldo % 8 == 0 && d->c_off % 8 == 0 && !(d->flags & FAC_CONV_OUT_F32) &&
       (!(d->flags & FAC_CONV_RESID) || (d->ldr % 8 == 0 && d->r_off % 8 == 0))) {
@@ -2424,28 +2364,20 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
 #undef FAC_PW
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
-  static const bool tk_ragged = [] {
-    const char* e = std::getenv("FAC_TK_RAGGED");
-    return !(e && e[0] == '0');
-  }();
   // S3D's temporal (kd,1,1) convs with 8 output frames: conv_tk (LDS slab per
   // 16 positions, the last one of a clip partial when 16 does not divide h*w)
   if (!split && d->kh == 1 && d->kw == 1 && d->sh == 1 && d->sw == 1 && d->ph == 0 && d->pw == 0 && d->od == 8 &&
-      d->cin % 64 == 0 && d->cout % 64 == 0 && (tk_ragged || (d->h * d->w) % 16 == 0) && d->ldo % 4 == 0 &&
+      d->cin % 64 == 0 && d->cout % 64 == 0 && d->ldo % 4 == 0 &&
       d->c_off % 4 == 0 &&
       (d->flags & ~FAC_CONV_RELU) == 0 && k_pad == d->kd * d->cin) {
     const int ks = d->kd * d->cin / 32, slab = d->d * 16 * d->cin;
     const int db = ks * 2048 + 2 * slab <= 81920 ? 2 : (ks * 2048 + slab <= 81920 ? 1 : 0);
-    static const bool tk2_on = [] {
-      const char* e = std::getenv("FAC_TK2");
-      return !(e && e[0] == '0');
-    }();
     const bool k3 = d->kd == 3 && d->sd == 1 && d->pd == 1 && d->d == 8;
     const bool k7 = d->kd == 7 && d->sd == 2 && d->pd == 3 && d->d == 16;
     // slices of KC 32-channel chunks (every chunk of a unit in one or two
     // steps: fewer per-step barriers and slice issues per MFMA), 3 ring slots
     const int tk2_kc = d->cin == 192 ? 3 : (d->cin == 128 ? 4 : 2);
-    if (tk2_on && (k3 || k7) && (d->cin == 64 || d->cin == 128 || d->cin == 192) &&
+    if ((k3 || k7) && (d->cin == 64 || d->cin == 128 || d->cin == 192) &&
         ks * 2048 + 128 + 3 * tk2_kc * d->d * 512 <= 81920 &&
         d->cin >= 64) {  // >= 2 slices per unit: at most R/2 store batches per wait window
       int dev = 0, ncu = 256;
@@ -2567,7 +2499,7 @@ static bool dual_convp(const fac_conv_desc* d, fac::ConvP& p, bool need_out) {
 int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stream) {
   using namespace fac;
   if (!d || !ds || d->dtype != ds->dtype || (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16)) return FAC_ERR_ARG;
-  if ((d->flags & (FAC_CONV_RESID | FAC_CONV_OUT_F32)) || ds->flags != 0) return FAC_ERR_ARG;
+  if ((d->flags & ~(FAC_CONV_RELU | FAC_CONV_RELU2)) || ds->flags != 0) return FAC_ERR_ARG;
   ConvP p, q;
   if (!dual_convp(d, p, true) || !dual_convp(ds, q, false)) return FAC_ERR_SHAPE;
   if (d->n != ds->n || d->od != ds->od || d->oh != ds->oh || d->ow != ds->ow || d->cout != ds->cout ||
@@ -2654,17 +2586,9 @@ int fac_pool_nd(const fac_pool_desc* d, void* stream) {
   const long long total = (long long)d->n * d->od * d->oh * d->ow * (d->c / 8);
   if (total >= (1LL << 31)) return FAC_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  static const bool mp3 = [] {
-    const char* e = std::getenv("FAC_POOL_MAX3");
-    return !(e && e[0] == '0');
-  }();
-  if (mp3 && d->mode == 0 && d->kd == 3 && d->kh == 3 && d->kw == 3 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+  if (d->mode == 0 && d->kd == 3 && d->kh == 3 && d->kw == 3 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
       d->pd == 1 && d->ph == 1 && d->pw == 1 && d->od == d->d && d->oh == d->h && d->ow == d->w) {
-    static const int zg_env = [] {  // output frames per thread (FAC_POOL_ZG; default: all of them)
-      const char* e = std::getenv("FAC_POOL_ZG");
-      return e ? std::atoi(e) : 0;
-    }();
-    const int zg = zg_env > 0 ? zg_env : d->d;
+    const int zg = d->d;  // output frames per thread: all of them
     const long long cols = (long long)d->n * ((d->d + zg - 1) / zg) * d->h * d->w * (d->c / 8);
     if (cols >= (1LL << 31)) return FAC_ERR_SHAPE;
     const int nb = (int)((cols + 255) / 256);

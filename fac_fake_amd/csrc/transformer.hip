@@ -394,6 +394,42 @@ __global__ __launch_bounds__(1024) void video_score(const float* __restrict__ lo
   *score = f > r ? f : fabsf(1.0f - r);
 }
 
+// Segmented video_score: one workgroup per video v over logits rows
+// [seg[v], seg[v+1]), the same sigmoid (expf) and the same sequential fp32
+// sums in crop order as video_score, so each video's score is bit-identical
+// to video_score on its own rows (several videos' crops scored in one batch,
+// cvit_prediction.py:73-83 run video by video in the reference).
+__global__ __launch_bounds__(256) void video_score_seg(const float* __restrict__ logits,
+                                                       const int* __restrict__ seg, int nv,
+                                                       float* __restrict__ score) {
+  constexpr int CAP = 1024;
+  __shared__ float sp[2 * CAP];
+  const int v = blockIdx.x;
+  if (v >= nv) return;
+  const int lo = seg[v], n = seg[v + 1] - lo;
+  float f = 0.f, r = 0.f;
+  for (int base = 0; base < n; base += CAP) {
+    const int m = n - base < CAP ? n - base : CAP;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * m; i += blockDim.x)
+      sp[i] = 1.0f / (1.0f + expf(-logits[2 * (size_t)(lo + base) + i]));
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 0; i < m; ++i) {
+        f += sp[2 * i];
+        r += sp[2 * i + 1];
+      }
+  }
+  if (threadIdx.x != 0) return;
+  if (n <= 2) {
+    score[v] = 0.5f;
+    return;
+  }
+  f = f / (float)n;
+  r = r / (float)n;
+  score[v] = f > r ? f : fabsf(1.0f - r);
+}
+
 }  // namespace fac
 
 namespace fac {
@@ -529,6 +565,11 @@ hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, f
 
 hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st) {
   video_score<<<1, 1024, 0, st>>>(logits, n, score);
+  return hipGetLastError();
+}
+
+hipError_t launch_video_score_seg(const float* logits, const int* seg, int nv, float* score, hipStream_t st) {
+  video_score_seg<<<nv, 256, 0, st>>>(logits, seg, nv, score);
   return hipGetLastError();
 }
 

@@ -10,7 +10,6 @@ every call goes through ``libfac_cvit.so`` and raises if it cannot.
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 
 import torch
@@ -343,20 +342,16 @@ def pool(x: torch.Tensor, kernel, stride, padding=0, mode: str = "max", out: tor
 
 def max_pool_sep(x: torch.Tensor, kernel, stride, padding=0) -> torch.Tensor:
     """Max pooling.  MaxPool3d(3, 1, 1) and strided windows are one
-    fac_pool_nd call (a sliding-window kernel / a direct pass); otherwise (or
-    with FAC_POOL_DIRECT=0 / FAC_POOL_MAX3=0) one fac_pool_nd pass per axis (W, then H, then D; axes
-    with kernel 1, stride 1 and no padding are skipped).  A max over a box
-    window (padding ignored, i.e. -inf) is the max over its rows of the max
-    over its columns, so the result is bit-identical to one 3-D pass, while
-    each output reads kw + kh + kd inputs instead of kw * kh * kd (27 -> 9
-    for S3D's 3x3x3 pools) and the strided axes shrink the later passes."""
+    fac_pool_nd call (a sliding-window kernel / a direct pass: for S3D's
+    (1,3,3)/(1,2,2), (3,3,3)/2, (2,2,2)/2 and ResNet's 3x3/2 one direct pass
+    over the 4-8x smaller output beat the separable passes, same-box S3D
+    29.4k -> 30.35k clips/s); other stride-1 windows are one fac_pool_nd pass
+    per axis (W, then H, then D; axes with kernel 1, stride 1 and no padding
+    are skipped).  A max over a box window (padding ignored, i.e. -inf) is
+    the max over its rows of the max over its columns, so every form is
+    bit-identical to one 3-D pass."""
     k, s, p = _triple(kernel), _triple(stride), _pads(padding)
-    if k == (3, 3, 3) and s == (1, 1, 1) and p == (1, 1, 1) and os.environ.get("FAC_POOL_MAX3", "1") != "0":
-        return pool(x, kernel, stride, padding, "max")  # fac_pool_nd's one-pass sliding-window kernel
-    if os.environ.get("FAC_POOL_DIRECT", "1") != "0" and s != (1, 1, 1):
-        # strided windows (S3D's (1,3,3)/(1,2,2), (3,3,3)/2, (2,2,2)/2, ResNet's
-        # 3x3/2): one direct pass over the 4-8x smaller output beats the
-        # separable passes (same-box S3D 29.4k -> 30.35k clips/s); bit-identical
+    if (k == (3, 3, 3) and s == (1, 1, 1) and p == (1, 1, 1)) or s != (1, 1, 1):
         return pool(x, kernel, stride, padding, "max")
     y = x
     for ax in (2, 1, 0):

@@ -28,14 +28,13 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import torch
 from torch import nn
 
 from . import _lib
 from .cvit import MAX_SLOTS, _Node, reference_mask_poisons
-from .ops import (TORCH16, ConvLayer, KANLinearLayer, bottleneck_pw2, conv_dual, fold_bn, max_pool_sep, pack_input_s2d,
+from .ops import (TORCH16, ConvLayer, KANLinearLayer, bottleneck_pw2, conv_dual, fold_bn, pack_input_s2d,
                   pool, s2d_weight, sigmoid)
 from .weights import kan_grid, resnet50_blocks, resvitkan_param_specs
 
@@ -187,35 +186,20 @@ class ResVitKan(nn.Module):
     # ms at 128 / 64 / 32 — the layers are not HBM-bound, the smaller grids
     # just fill the 256 CUs worse (tools/rvk_chunks.sh)
     feature_chunk = 0
-    side_downsample = os.environ.get("FAC_RVK_SIDE", "1") != "0"
-    fuse_downsample = os.environ.get("FAC_RVK_DUAL", "1") != "0"
-    # conv1 + bn1 + relu + maxpool as one launch (conv_s2d4_mp); FAC_RVK_MP=0:
-    # conv_s2d4 then fac_pool_nd
-    fuse_maxpool = os.environ.get("FAC_RVK_MP", "1") != "0"
-    # a layer1 bottleneck's conv3 and the next block's conv1 as one launch
-    # (fac_bottleneck_pw2); FAC_RVK_PW2=0: two launches
-    fuse_pw2 = os.environ.get("FAC_RVK_PW2", "1") != "0"
-    # layer2's pairs too (bneck_pw2_l2): correct but measured slower than the
-    # two launches (69.3k vs 69.7-69.9k crops/s same box), so opt-in
-    fuse_pw2_l2 = os.environ.get("FAC_RVK_PW2_L2", "0") == "1"
+    # a layer1 bottleneck's conv3 and the next block's conv1 run as one launch
+    # (fac_bottleneck_pw2).  Layer2's pairs stay two launches: the fused
+    # layer2 kernel (bneck_pw2_l2) is correct but measured slower (69.3k vs
+    # 69.7-69.9k crops/s same box).
 
     @staticmethod
     def _pw2_ok(c3, c1n, x) -> bool:
         """fac_bottleneck_pw2's shapes: conv3 1x1 64 -> 256, the next conv1 1x1
         256 -> 64 / 128 at stride 1 (torchvision v1.5 puts the stride on conv2)."""
         g3, g1 = c3.g, c1n.g
-        shapes = ((c3.cin == 64 and c3.cout == 256 and c1n.cin == 256 and c1n.cout in (64, 128))
-                  or (c3.cin == 128 and c3.cout == 512 and c1n.cin == 512 and c1n.cout == 128 and ResVitKan.fuse_pw2_l2))
+        shapes = c3.cin == 64 and c3.cout == 256 and c1n.cin == 256 and c1n.cout in (64, 128)
         return (shapes and (g3.kd, g3.kh, g3.kw, g3.sd, g3.sh, g3.sw) == (1,) * 6
                 and (g1.kd, g1.kh, g1.kw, g1.sd, g1.sh, g1.sw) == (1,) * 6
                 and (g1.pd, g1.ph, g1.pw) == (0, 0, 0) and x.shape[-1] == c3.cout)
-
-    def _side_stream(self, device: torch.device):
-        st = getattr(self, "_side", None)
-        if st is None or st.device != device:
-            st = torch.cuda.Stream(device)
-            self._side = st
-        return st
 
     def features16(self, x16: torch.Tensor, out: torch.Tensor | None = None, taps: list | None = None) -> torch.Tensor:
         """ResNet.forward (ResVitKan.py:232-247) on space-to-depth packed 16-bit
@@ -229,43 +213,28 @@ class ResVitKan(nn.Module):
         step = B if taps is not None else (self.feature_chunk or B)
         tap = taps.append if taps is not None else (lambda t: None)
         for b0 in range(0, B, step):
-            if self.fuse_maxpool:
-                # 7x7/2 + bn1 + ReLU + MaxPool2d(3, 2, 1) in one launch (conv_s2d4_mp)
-                x = self._conv1(x16[b0:b0 + step], maxpool3s2=True)
-            else:
-                x = self._conv1(x16[b0:b0 + step])                  # 7x7/2 + bn1 + ReLU, on s2d cells
-                x = max_pool_sep(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))  # MaxPool2d(3, 2, 1)
+            # 7x7/2 + bn1 + ReLU + MaxPool2d(3, 2, 1) in one launch (conv_s2d4_mp)
+            x = self._conv1(x16[b0:b0 + step], maxpool3s2=True)
             tap(x)
             h1 = None  # the next block's conv1 output, when the previous conv3 computed it
             for bi, (c1, c2, c3, ds) in enumerate(self._blocks):
                 nxt = self._blocks[bi + 1] if bi + 1 < len(self._blocks) else None
-                if ds is None and self.fuse_pw2 and nxt is not None and self._pw2_ok(c3, nxt[0], x):
+                if ds is None and nxt is not None and self._pw2_ok(c3, nxt[0], x):
                     # conv3 (+ identity residual) and the next block's conv1 in
                     # one launch (fac_bottleneck_pw2): x is not read back
                     x, h1n = bottleneck_pw2(c3, c2(h1 if h1 is not None else c1(x)), x, nxt[0])
                     h1 = h1n
                     tap(x)
                     continue
-                if ds is not None and self.fuse_downsample:
+                if ds is not None:
                     # conv3 + bn3 + ReLU and the downsample conv + bn in one launch
                     # (fac_conv_nd_dual): the residual never goes through memory
                     x = conv_dual(c3, c2(h1 if h1 is not None else c1(x)), ds, x)
                     h1 = None
                     tap(x)
                     continue
-                if ds is not None and self.side_downsample:
-                    # the downsample branch (first block of each layer) runs on a
-                    # side stream beside conv1 -> conv2, joined before conv3 adds it
-                    main = torch.cuda.current_stream(x.device)
-                    side = self._side_stream(x.device)
-                    side.wait_stream(main)
-                    with torch.cuda.stream(side):
-                        res = ds(x, relu=False)
-                    h = c2(h1 if h1 is not None else c1(x))
-                    main.wait_stream(side)
-                else:
-                    res = x if ds is None else ds(x, relu=False)
-                    h = c2(h1 if h1 is not None else c1(x))
+                res = x
+                h = c2(h1 if h1 is not None else c1(x))
                 h1 = None
                 x = c3(h, residual=res, relu2=True)                 # relu(bn3) + residual, relu
                 tap(x)

@@ -22,7 +22,6 @@ Arithmetic (every layer a HIP kernel of libfac_cvit.so, no CPU fallback):
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 from torch import nn
@@ -155,7 +154,7 @@ class S3D(nn.Module):
                 # convs reading them take K steps that each lie in one tap
                 # (convnd_igemm's uniform-tap gather)
                 p1, p2 = self._pad64(b1a, 1), self._pad64(b2a, 2)
-                # and (FAC_S3D_PADT) the SepConvs' middle channels, so their
+                # and (padt) the SepConvs' middle channels, so their
                 # (3,1,1) halves take the uniform-tap gather too
                 m1 = (b1b + 63) // 64 * 64 if self.padt else b1b
                 m2 = (b2b + 63) // 64 * 64 if self.padt else b2b
@@ -166,8 +165,7 @@ class S3D(nn.Module):
                     merged_p = ConvLayer(torch.cat(hw), torch.cat(hb), 1, 0, dtype=dt, device=device)
                 b1, b2 = sep(f"{p}.branch1.1", 3, 1, 1), sep(f"{p}.branch2.1", 3, 1, 1)
                 self._layers.append(("mixed", dict(
-                    b0=bconv(f"{p}.branch0.0"), b1a=bconv(f"{p}.branch1.0"), b1=b1,
-                    b2a=bconv(f"{p}.branch2.0"), b2=b2, b3=bconv(f"{p}.branch3.1"),
+                    b1=b1, b2=b2, b3=bconv(f"{p}.branch3.1"),
                     b1p=b1 if (p1, m1) == (b1a, b1b) else sep(f"{p}.branch1.1", 3, 1, 1, cin_pad=p1, mid_pad=m1),
                     b2p=b2 if (p2, m2) == (b2a, b2b) else sep(f"{p}.branch2.1", 3, 1, 1, cin_pad=p2, mid_pad=m2),
                     heads=merged, head_splits=(b0, b0 + b1a), head_widths=(b1a, b2a),
@@ -177,86 +175,43 @@ class S3D(nn.Module):
         self._prep = (idx, v)
 
     # ------------------------------------------------------------------ forward
-    # Opt-in (FAC_S3D_CONCURRENT=1, side-stream priority FAC_S3D_SIDE_PRIORITY,
-    # default -1).  Whether the overlap pays depends on which of the process's
-    # four hardware queues torch's pool streams land on, i.e. on the process's
-    # stream history: normal-priority side streams ran the graph at 27.0k
-    # clips/s alone in a process but 20.5k after the CViT bench (serial 24.9k);
-    # priority -1 gave 27.2k after the CViT bench (serial 26.2k) but 20.8k
-    # alone.  Serial is the dependable default.
-    concurrent_branches = os.environ.get("FAC_S3D_CONCURRENT", "0") == "1"
-    # serial order: the three 1x1x1 heads as one column-split launch (ops.conv_split)
-    merged_heads = os.environ.get("FAC_S3D_MERGED_HEADS", "1") == "1"
     # channel padding of the merged heads' branch1.0 / branch2.0 outputs to a
     # multiple of 64: 0 none, 1 branch1.0 when >= 64 channels, 2 both
-    pad64_level = int(os.environ.get("FAC_S3D_PAD64", "1"))
-    padt = os.environ.get("FAC_S3D_PADT", "1") == "1"
+    # (level 1 measured fastest); and the SepConvs' middle channels to a
+    # multiple of 64 (padt), so their (3,1,1) halves take the uniform-tap gather
+    pad64_level = 1
+    padt = True
 
     def _pad64(self, c: int, level: int) -> int:
         if self.pad64_level < level or c % 64 == 0 or (level == 1 and c < 64):
             return c
         return (c + 63) // 64 * 64
 
-    def _branch_streams(self, device: torch.device):
-        """Three side streams (per device) for the Inception branches."""
-        streams = getattr(self, "_side", None)
-        if streams is None or streams[0].device != device:
-            prio = int(os.environ.get("FAC_S3D_SIDE_PRIORITY", "-1"))
-            streams = [torch.cuda.Stream(device, priority=prio) for _ in range(3)]
-            self._side = streams
-        return streams
-
     def _mixed(self, x, blk):
-        """One Mixed_* block (model.py:84-342).  Its four branches read the same
-        input and write disjoint channel slots of the block output, so they
-        run concurrently: branch 0 on the current stream, branches 1-3 on side
-        streams forked from it and joined back before the output is used (a
-        hipGraph capture turns this into four parallel chains of nodes).  The
-        late blocks' launches are latency-bound (4x7 and 2x3 maps: 100-200
-        workgroups each), so overlapping the chains shortens the block instead
-        of leaving most CUs idle between dependent launches."""
+        """One Mixed_* block (model.py:84-342).  Its four branches read the
+        same input and write disjoint channel slots of the block output: the
+        three 1x1x1 heads (branch0.0, branch1.0, branch2.0) as one
+        column-split launch (ops.conv_split: branch0 straight into its slot),
+        then branch1's and branch2's SepConvs, then branch3's MaxPool3d(3,1,1)
+        + 1x1x1.  (The branches on concurrent side streams measured faster or
+        slower depending on which hardware queues torch's pool streams land on
+        -- 27.0k vs 20.5k clips/s for the same graph -- so the serial order is
+        the dependable one.)"""
         n, d, h, w, _ = x.shape
         out = torch.empty(n, d, h, w, sum(blk["widths"]), dtype=x.dtype, device=x.device)
         o1 = blk["widths"][0]
         o2 = o1 + blk["widths"][1]
         o3 = o2 + blk["widths"][2]
-        main = torch.cuda.current_stream(x.device)
-        if not self.concurrent_branches and not self.merged_heads:
-            s1, t1 = blk["b1"]
-            s2, t2 = blk["b2"]
-            blk["b0"](x, out=out, c_off=0)
-            t1(s1(blk["b1a"](x)), out=out, c_off=o1)
-            t2(s2(blk["b2a"](x)), out=out, c_off=o2)
-            blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
-            return out
-        if not self.concurrent_branches:
-            sfx = "_p" if h < 14 else ""   # channel-padded heads (pad64_level) where no conv.hip tile exists
-            s1, t1 = blk["b1p" if sfx else "b1"]
-            s2, t2 = blk["b2p" if sfx else "b2"]
-            # branch0 into its slot, branch1.0 / branch2.0 into their own
-            # tensors: one launch (column-split GEMM) instead of three
-            hws = blk["head_widths" + sfx]
-            h1 = torch.empty(n, d, h, w, hws[0], dtype=x.dtype, device=x.device)
-            h2 = torch.empty(n, d, h, w, hws[1], dtype=x.dtype, device=x.device)
-            conv_split(blk["heads" + sfx], x, blk["head_splits" + sfx], out, 0, h1, h2)
-            t1(s1(h1), out=out, c_off=o1)
-            t2(s2(h2), out=out, c_off=o2)
-            blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
-            return out
-        side = self._branch_streams(x.device)
-        for s in side:
-            s.wait_stream(main)
-        with torch.cuda.stream(side[0]):
-            s1, t1 = blk["b1"]
-            t1(s1(blk["b1a"](x)), out=out, c_off=o1)
-        with torch.cuda.stream(side[1]):
-            s2, t2 = blk["b2"]
-            t2(s2(blk["b2a"](x)), out=out, c_off=o2)
-        with torch.cuda.stream(side[2]):
-            blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)   # MaxPool3d(3, 1, 1) then 1x1x1
-        blk["b0"](x, out=out, c_off=0)
-        for s in side:
-            main.wait_stream(s)
+        sfx = "_p" if h < 14 else ""   # channel-padded heads (pad64_level) where no conv.hip tile exists
+        s1, t1 = blk["b1p" if sfx else "b1"]
+        s2, t2 = blk["b2p" if sfx else "b2"]
+        hws = blk["head_widths" + sfx]
+        h1 = torch.empty(n, d, h, w, hws[0], dtype=x.dtype, device=x.device)
+        h2 = torch.empty(n, d, h, w, hws[1], dtype=x.dtype, device=x.device)
+        conv_split(blk["heads" + sfx], x, blk["head_splits" + sfx], out, 0, h1, h2)
+        t1(s1(h1), out=out, c_off=o1)
+        t2(s2(h2), out=out, c_off=o2)
+        blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
         return out
 
     def features16(self, x16: torch.Tensor, taps: list | None = None) -> torch.Tensor:

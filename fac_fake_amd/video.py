@@ -76,13 +76,21 @@ def synthetic_video(n_frames: int, height: int = 1080, width: int = 1920, seed: 
     return frames, boxes
 
 
-def crop_faces(frames: torch.Tensor, boxes) -> torch.Tensor:
-    """uint8 BGR frames [F, H, W, 3] (device) + boxes [n, 5] -> uint8 RGB crops [n, 224, 224, 3] (device)."""
+def crop_faces(frames: torch.Tensor, boxes, out: torch.Tensor | None = None) -> torch.Tensor:
+    """uint8 BGR frames [F, H, W, 3] (device) + boxes [n, 5] -> uint8 RGB crops
+    [n, 224, 224, 3] (device; written into ``out`` when given, a contiguous
+    [n, 224, 224, 3] uint8 tensor on the frames' device)."""
     if not frames.is_cuda or frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
         raise ValueError("frames must be a uint8 [F, H, W, 3] device tensor")
     b = torch.as_tensor(np.asarray(boxes, dtype=np.int32).reshape(-1, 5)).to(frames.device)
     n = int(b.shape[0])
-    crops = torch.empty(n, CROP, CROP, 3, dtype=torch.uint8, device=frames.device)
+    if out is None:
+        crops = torch.empty(n, CROP, CROP, 3, dtype=torch.uint8, device=frames.device)
+    else:
+        if (out.dtype != torch.uint8 or tuple(out.shape) != (n, CROP, CROP, 3) or not out.is_contiguous()
+                or out.device != frames.device):
+            raise ValueError(f"out must be a contiguous uint8 [{n},{CROP},{CROP},3] tensor on {frames.device}")
+        crops = out
     if n:
         frames = frames.contiguous()
         F, H, W, _ = frames.shape
@@ -148,6 +156,97 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         raise ValueError("mode must be 'reference' or 'dense'")
     score = device_video_score(logits)
     return (score, logits) if return_logits else score
+
+
+def select_reference(frames, boxes):
+    """The reference's crop selection for one video (``reference_boxes``) and
+    the frames it needs: ``(frames, sel)`` with ``sel`` [n, 5] indexing into
+    the returned frames.  A device tensor is returned as is; a host video
+    (numpy array / CPU tensor) is cut down to the frames the schedule reads
+    (int(0.1 * F) reads, :165-198: ~30 frames of a 300-frame 1080p video,
+    187 MB instead of 1.87 GB to hold and to upload)."""
+    sel = reference_boxes(boxes, int(frames.shape[0]))
+    if isinstance(frames, torch.Tensor) and frames.is_cuda:
+        return frames, sel
+    ids, inv = np.unique(sel[:, 0], return_inverse=True)
+    sub = np.asarray(frames)[ids.astype(np.int64)] if len(sel) else np.zeros((0, 1, 1, 3), np.uint8)
+    sel = sel.copy()
+    sel[:, 0] = inv.reshape(-1).astype(np.int32)
+    return sub, sel
+
+
+def score_selected(model, items, batch: int = 256, device=None, return_logits: bool = False):
+    """Reference-mode scores of videos whose crops are already selected:
+    ``items`` = [(frames, sel)] as ``select_reference`` returns them.  Each
+    video keeps its own chunk slots 0..n-1 (``chunk_slots``); the crops of
+    all videos are concatenated, scored in forwards of at most ``batch``
+    crops (pipelined: batch k's encoder beside batch k+1's conv stack), and
+    reduced per video by one ``fac_video_score_seg`` launch."""
+    items = list(items)
+    if not items:
+        return ([], None) if return_logits else []
+    dev = torch.device(device) if device is not None else None
+    if dev is None:
+        for fr, _ in items:
+            if isinstance(fr, torch.Tensor) and fr.is_cuda:
+                dev = fr.device
+                break
+        else:
+            dev = torch.device("cuda", torch.cuda.current_device())
+    seg = np.zeros(len(items) + 1, dtype=np.int32)
+    np.cumsum([len(sel) for _, sel in items], out=seg[1:])
+    total = int(seg[-1])
+    crops = torch.empty(total, CROP, CROP, 3, dtype=torch.uint8, device=dev)
+    pos = np.zeros(total, dtype=np.int32)
+    for v, (frames, sel) in enumerate(items):
+        if len(sel) == 0:
+            continue
+        fr = frames if isinstance(frames, torch.Tensor) and frames.is_cuda else \
+            torch.as_tensor(np.ascontiguousarray(frames)).to(dev)
+        crop_faces(fr, sel, out=crops[seg[v]:seg[v + 1]])
+        pos[seg[v]:seg[v + 1]] = chunk_slots(len(sel))
+    with torch.no_grad():
+        if total == 0:
+            logits = torch.zeros(0, 2, dtype=torch.float32, device=dev)
+        elif total <= batch:
+            logits = model.forward_u8(crops, pos_index=torch.from_numpy(pos))
+        else:
+            logits = model.forward_u8_pipelined(crops, torch.from_numpy(pos), chunk=batch, equal=False)
+    scores = segmented_video_scores(logits, seg)
+    return (scores, logits) if return_logits else scores
+
+
+def predict_videos(model, videos, batch: int = 256, device=None, return_logits: bool = False):
+    """Reference-mode scores of several videos (cvit_prediction.py:73-83 runs
+    ``predict`` video after video, one <= 29-crop forward each), with the
+    crops of many videos in one forward.
+
+    ``videos``: iterable of ``(frames, boxes)``: decoded BGR uint8 frames
+    [F, H, W, 3] (device tensor, or host array / CPU tensor: only the frames
+    the schedule reads are uploaded) and boxes [n, 5] (frame, left, top,
+    right, bottom).  A crop's logits do not depend on its batch (fixed
+    split-K orders, no cross-crop op before the score) and the segmented
+    score sums each video's sigmoids in crop order, so every score is
+    bit-identical to ``predict_video(model, frames, boxes)``.  Returns a list
+    of floats (and the [N, 2] logits with ``return_logits``).
+    """
+    return score_selected(model, [select_reference(f, b) for f, b in videos], batch, device, return_logits)
+
+
+def segmented_video_scores(logits: torch.Tensor, seg) -> list:
+    """Per-video ``pre_process_prediction(pred_sig(.))`` of logit rows
+    [seg[v], seg[v+1]) (fac_video_score_seg), one device->host read."""
+    seg = np.asarray(seg, dtype=np.int32)
+    nv = len(seg) - 1
+    if nv <= 0:
+        return []
+    logits = logits.float().contiguous()
+    d_seg = torch.from_numpy(seg).to(logits.device)
+    out = torch.empty(nv, dtype=torch.float32, device=logits.device)
+    _lib.check(_lib.load().fac_video_score_seg(logits.data_ptr(), d_seg.data_ptr(), nv, out.data_ptr(),
+                                               torch.cuda.current_stream(logits.device).cuda_stream),
+               None, "fac_video_score_seg")
+    return [float(s) for s in out.cpu().tolist()]
 
 
 def device_video_score(logits: torch.Tensor) -> float:

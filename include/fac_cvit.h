@@ -157,6 +157,14 @@ int fac_check_device_errors(fac_ctx* ctx, int* flags);
  * cvit_prediction.py:240,258-281): d_score = fp32 scalar. */
 int fac_video_score(const float* d_logits, int n, float* d_score, void* stream);
 
+/* The same score for nv videos whose crops were scored in one batch:
+ * video v owns logit rows [d_seg[v], d_seg[v+1]) (int32 [nv+1], device,
+ * non-decreasing); d_scores = fp32 [nv].  Each score is bit-identical to
+ * fac_video_score on that video's rows alone (same sigmoid, same fp32 sums in
+ * crop order).  Replaces predict_on_video's one-video-at-a-time loop
+ * (cvit_prediction.py:73-83) with batched forwards. */
+int fac_video_score_seg(const float* d_logits, const int* d_seg, int nv, float* d_scores, void* stream);
+
 /* Face crops of config 3 (cvit_prediction.py:111-116): for each box
  * (frame, left, top, right, bottom) in d_boxes (int32 [n_boxes][5]), take
  * frame[top:bottom, left:right] of the BGR uint8 frames [n_frames][H][W][3],
@@ -178,8 +186,8 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * of to_out and FF2: 1, 2 or 4), "tail_only" (before fac_load_weights: no
  * conv stem, fac_forward_features only), "tail_priority", "stem_events" (1 =
  * time every fused-stem launch, fac_stem_event_ms), "stem_dynamic" (1 =
- * the fused stem claims boxes from a device counter, the default; 0 = static
- * box schedule), "stem_nwg" (persistent fused-stem workgroups; 0 = one per
+ * the fused stem claims boxes from a device counter; 0 = static box
+ * schedule, the default), "stem_nwg" (persistent fused-stem workgroups; 0 = one per
  * CU, the default), "ffn_ln_eps_exp" (n:
  * the FeedForward PreNorm LayerNorm uses eps = 10^-n; default 5, the RepBn8
  * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48). */

@@ -38,6 +38,25 @@ def golden():
     return _load
 
 
+ENVELOPE_MARGIN = 1.25
+
+
+@pytest.fixture(scope="session")
+def tol16():
+    """End-to-end probability tolerance of a golden fixture: fp16 at the
+    north-star bar (1e-3); bf16 at 1.25x the oracle's emulated bf16 rounding
+    envelope on that fixture's own inputs (tests/golden/bf16_envelope.json,
+    tools/bf16_envelope.py), so a bf16-only regression cannot hide in a flat
+    1e-2."""
+    env = json.loads((GOLDEN / "bf16_envelope.json").read_text())
+
+    def _tol(dt, fixture):
+        if dt == "fp16":
+            return 1e-3
+        return ENVELOPE_MARGIN * env["bf16"][fixture]
+    return _tol
+
+
 @pytest.fixture(scope="session", autouse=True)
 def built_lib():
     """(Re)build libfac_cvit.so when any source is newer than it (mtime-checked,

@@ -65,6 +65,10 @@ def test_predict_on_video_end_to_end(tmp_path):
     cp.sample = str(tmp_path)
     got = cp.predict_on_video(names, num_workers=1)
     assert got == want and got[2] == 0.5
+    # several reader threads, and groups smaller than the videos' crop total
+    # (one forward per video): the same scores, in order
+    assert cp.predict_on_video(names, num_workers=3) == want
+    assert cp.predict_on_video(names, num_workers=2, batch=8) == want
     out = cp.write_predictions(names, got, tmp_path / "pred.csv")
     rows = out.read_text().splitlines()
     assert rows[0] == "filename,label" and len(rows) == 4

@@ -8,8 +8,9 @@
 * fac_pool_nd: bit-exact (max) / within fp32 rounding of one 16-bit ulp (avg).
 * fac_kan_linear vs the reference's KANLinear outputs (golden): <= 1e-5.
 * ResVitKan forward vs the reference module's logits (golden, fp32):
-  per-logit sigmoid within 1e-3 with fp16 operands and 1e-2 with bf16
-  (the emulated rounding alone moves bf16 by ~2e-3, tests/test_resvitkan.py).
+  per-logit sigmoid within 1e-3 with fp16 operands and, with bf16, within
+  1.25x the oracle's emulated bf16 envelope on the same inputs (1.9e-3 for
+  ResVitKan, 0.8-1.0e-3 for S3D: tests/golden/bf16_envelope.json).
 """
 import numpy as np
 import pytest
@@ -309,9 +310,10 @@ def rvk():
     return out
 
 
-@pytest.mark.parametrize("dt,tol", [("fp16", 1e-3), ("bf16", 1e-2)])
-def test_resvitkan_matches_reference(rvk, golden, dt, tol):
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_resvitkan_matches_reference(rvk, golden, dt, tol16):
     from oracle.cvit_torch import normalize_u8
+    tol = tol16(dt, "resvitkan_golden.npz")
     g = golden("resvitkan_golden.npz")
     crops = make_crops(4, seed=int(g["crop_seed"]))
     m = rvk[dt]
@@ -400,9 +402,10 @@ def s3d_models():
 
 
 @pytest.mark.parametrize("srm", ["no", "yes"])
-@pytest.mark.parametrize("dt,tol", [("fp16", 1e-3), ("bf16", 1e-2)])
-def test_s3d_matches_reference(s3d_models, golden, srm, dt, tol):
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_s3d_matches_reference(s3d_models, golden, srm, dt, tol16):
     """Per-logit sigmoid of 2 raw 16x112x112 clips vs the reference module (golden)."""
+    tol = tol16(dt, f"s3d_golden.npz:{srm}")
     from fac_fake_amd.weights import s3d_clips
     g = golden("s3d_golden.npz")
     x = torch.from_numpy(s3d_clips(2, 16, 112, seed=int(g["clip_seed"]))).to(DEV)

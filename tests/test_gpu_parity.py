@@ -4,9 +4,10 @@ Tolerances (stated per test):
 * fp16 operands: per-frame probabilities within 1e-3 of the fp32 reference
   (the north-star bar), checked against goldens the reference produced.
 * bf16 operands: exact bf16 rounding of the operands alone already moves the
-  fp32 reference by up to ~4e-3 in probability on these weights (oracle
-  emulation; DESIGN.md "bf16 vs the 1e-3 bar"), so end-to-end bf16 is gated
-  at 1e-2 against the fp32 goldens, and the kernels themselves are gated
+  fp32 reference by 1.5e-3 .. 5.3e-3 in probability on these fixtures (the
+  oracle's emulation, tests/golden/bf16_envelope.json), so
+  end-to-end bf16 is gated at 1.25x that envelope per fixture (conftest
+  tol16), and the kernels themselves are gated
   tightly per kernel: each conv fed the oracle's previous-layer output agrees
   to <= 2 ulp (1-ulp accumulation-order flips on a few % of outputs), the
   tail fed the oracle's stem output agrees within 1e-3 in probability, and
@@ -57,41 +58,41 @@ def test_native_library_is_the_one_loaded(models):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_c1_single_crop(models, golden, dt):
+def test_c1_single_crop(models, golden, dt, tol16):
     g = golden("golden_c1.npz")
     crops = make_crops(1, seed=1)
     assert int(crops.astype(np.int64).sum()) == int(g["crop_sum"])
     lg = _run_u8(models[dt], crops, [0])
     dp = np.abs(_sig(lg) - g["probs"]).max()
     assert np.isfinite(lg).all()
-    assert dp <= (1e-3 if dt == "fp16" else 1e-2), (dt, dp, lg, g["logits"])
+    assert dp <= tol16(dt, "golden_c1.npz"), (dt, dp, lg, g["logits"])
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_b32_all_slots(models, golden, dt):
+def test_b32_all_slots(models, golden, dt, tol16):
     g = golden("golden_b32.npz")
     crops = make_crops(32, seed=2)
     lg = _run_u8(models[dt], crops, np.arange(32))
     dp = np.abs(_sig(lg) - _sig(g["logits"])).max()
-    assert dp <= (1e-3 if dt == "fp16" else 1e-2), (dt, dp)
+    assert dp <= tol16(dt, "golden_b32.npz"), (dt, dp)
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_b256_config2(models, golden, dt):
+def test_b256_config2(models, golden, dt, tol16):
     """Config 2: B=256 crops in one call, slot = j mod 32 (8 reference chunks of 32)."""
     g = golden("golden_b256.npz")
     crops = make_crops(256, seed=3)
     lg = _run_u8(models[dt], crops, np.arange(256) % 32)
     dp = np.abs(_sig(lg) - _sig(g["logits"])).max()
-    assert dp <= (1e-3 if dt == "fp16" else 1e-2), (dt, dp)
+    assert dp <= tol16(dt, "golden_b256.npz"), (dt, dp)
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_real_crops(models, golden, dt):
+def test_real_crops(models, golden, dt, tol16):
     g = golden("golden_real.npz")
     lg = _run_u8(models[dt], g["crops"], [0, 1])
     dp = np.abs(_sig(lg) - _sig(g["logits"])).max()
-    assert dp <= (1e-3 if dt == "fp16" else 1e-2), (dt, dp)
+    assert dp <= tol16(dt, "golden_real.npz"), (dt, dp)
 
 
 ULP_REL = {"fp16": 2.0 ** -10, "bf16": 2.0 ** -7}  # one unit in the last place, relative
@@ -529,6 +530,33 @@ def test_video_driver_matches_drop_in(models, mode):
     # the score is computed on the device (fac_video_score): the reference's
     # rule, up to the sigmoid's last-bit rounding
     assert abs(score - float(pre_process_prediction(pred_sig(ref)))) <= 1e-6
+
+
+def test_multi_video_batching_matches_per_video(models):
+    """predict_videos (config 3's reference workload, cvit_prediction.py:73-83:
+    <= 29 crops per video, slots 0..n-1 each) scores many videos' crops in
+    shared forwards and reduces them with one segmented score launch: every
+    score and every logit is bit-identical to predict_video on that video
+    alone, for videos with 0, 1, 2, 3 and 29 crops, host and device frames,
+    and batches that split videos across forwards."""
+    from fac_fake_amd.video import predict_video, predict_videos, synthetic_video
+    m = models["bf16"]
+    vids = []
+    for i, (n, faces) in enumerate(((300, 1), (40, 1), (10, 1), (20, 1), (30, 1), (120, 3), (7, 1), (60, 2))):
+        frames, boxes = synthetic_video(n, 270, 480, seed=11 + i, device=DEV, faces_per_frame=faces, box_min=40,
+                                        box_span=200)
+        if i == 6:
+            boxes = boxes[:0]
+        vids.append((frames, boxes))
+    want, want_lg = zip(*[predict_video(m, f, b, mode="reference", return_logits=True) for f, b in vids])
+    counts = [0 if lg is None else lg.shape[0] for lg in want_lg]
+    assert {0, 1, 2, 3, 29} <= set(counts), counts
+    ref_lg = torch.cat([lg for lg in want_lg if lg is not None]).cpu()
+    for batch, host in ((256, False), (32, False), (7, True)):
+        src = [(f.cpu().numpy(), b) if host else (f, b) for f, b in vids]
+        got, lg = predict_videos(m, src, batch=batch, device=DEV, return_logits=True)
+        assert got == list(want), (batch, got, want)
+        assert torch.equal(lg.cpu(), ref_lg), batch
 
 
 def test_stem_event_timing(models):

@@ -75,6 +75,9 @@ def test_conv_nd_dual_argument_checks(built_lib):
     r = desc(128, 28, 1)
     r.flags = 2                                                                   # FAC_CONV_RESID
     assert lib.fac_conv_nd_dual(C.byref(r), C.byref(b), None) == -1
+    for f in (8, 16, 32, 1 | 16):                      # OUT_F32, MAXPOOL3S2, an undefined bit, RELU | MAXPOOL3S2
+        r.flags = f
+        assert lib.fac_conv_nd_dual(C.byref(r), C.byref(b), None) == -1, f
     assert lib.fac_conv_nd_dual(C.byref(desc(96, 28, 1)), C.byref(b), None) == -2  # cin % 64
     assert lib.fac_conv_nd_dual(C.byref(a), C.byref(desc(256, 56, 1)), None) == -2  # 56x56 vs 28x28 outputs
     assert lib.fac_conv_nd_dual(C.byref(a), C.byref(desc(256, 56, 2, cout=128)), None) == -2  # cout differs
@@ -255,3 +258,13 @@ def test_reference_mask_semantics(golden):
             assert reference_mask_poisons(mask, c["B"]) == (c["outcome"] == "nan"), c
             if c["outcome"] == "nan":
                 assert all(c["nan_rows"])
+
+
+def test_segmented_score_argument_checks(built_lib):
+    """fac_video_score_seg rejects a negative count and null buffers, and an
+    empty segment list is a no-op; none of these cases touches the device."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    assert lib.fac_video_score_seg(None, None, -1, None, None) == -1
+    assert lib.fac_video_score_seg(None, None, 0, None, None) == 0
+    assert lib.fac_video_score_seg(None, None, 2, None, None) == -1
