@@ -41,6 +41,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                    (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
+// value of lane (quad_perm CTRL) within each group of 4 lanes (DPP, no LDS)
+template <int CTRL>
+__device__ __forceinline__ float quad_perm_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
 template <int TW>
 constexpr int halo_rp() { return TW + 2 <= 24 ? 24 : 40; }
 
@@ -80,15 +86,14 @@ __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, 
 // 1: it is loaded between chunks, exposed, which halves the halo LDS so that
 // OCC = 3 workgroups share a CU and hide each other's exposed loads — the
 // 112^2 layers, whose 1-2 chunks leave little to pipeline within a box).
-//
-// NBOX = 2: an 8-wave workgroup computes two boxes (waves 4k..4k+3 box k, each
-// exactly as a 4-wave workgroup would, with its own halo buffers) that share
-// the per-tap weight slices: half the weight glds per MFMA (a 1 KB wave load
-// costs ~46 SIMD cycles beside MFMAs, tools/ubench/issue_ubench.hip), at the
-// price of one barrier across both boxes.
+// TR: transposed MFMA (D^T = W . A^T: weights as the A operand, pixels as B),
+// so each lane holds 4 consecutive output channels of one pixel and the
+// epilogue stores them straight to NHWC global memory (8 bytes per lane, the
+// 2x2 max-pool across the 4 lanes of a window by DPP) instead of 2-byte LDS
+// staging writes, a barrier and a raster copy.
 template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
-          int NBOX = 1>
-__global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
+          bool TR = false>
+__global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
@@ -125,18 +130,15 @@ __global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_
   constexpr int WSL = BN * CK;              // elements per tap slice
   constexpr int OPIX = POOL ? NPIX / 4 : NPIX;
   constexpr int OPS = BN + 8;
-  constexpr int OPER = NBOX * HB * HALO + 3 * WSL;   // halo buffer(s) per box + 3-slot weight ring
-  constexpr int OSTGB = (POOL ? RT * 4 : RT * 16) * OPS;  // per box, padded: epilogue writes unguarded
-  constexpr int OSTG = NBOX * OSTGB;
+  constexpr int OPER = HB * HALO + 3 * WSL;   // halo buffer(s) + 3-slot weight ring
+  constexpr int OSTG = (POOL ? RT * 4 : RT * 16) * OPS;  // padded: epilogue writes unguarded
   constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
   static_assert(WM * WN == 4, "4 waves");
   static_assert(TH % 2 == 0 && TW % 2 == 0, "window-major order needs even boxes");
   static_assert(CTW * 16 * WN == BN, "BN split");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
-  // box-local thread / wave (everything but the shared weight ring), box index
-  const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
-  const int wave_g = threadIdx.x >> 6, box = NBOX > 1 ? (int)(threadIdx.x >> 8) : 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
   // XCD-aware box order: workgroups are dealt round-robin to the 8 XCDs
@@ -146,7 +148,6 @@ __global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_
   // 1.27x halo overhead with the plain order).
   int bx = blockIdx.x;
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  bx = bx * NBOX + box;
   const int b = bx / tiles_per_img;
   const int tile = bx - b * tiles_per_img;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
@@ -199,16 +200,14 @@ __global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_
   // slice in memory IS its LDS image, so wave w copies pieces
   // [256i + 64w, +64) straight into ring slot `slot`.
   constexpr int WPIECES = BN * CK / 8;
-  constexpr int WPT = 256 * NBOX;              // threads loading a slice
-  constexpr int WPW = (WPIECES + WPT - 1) / WPT;  // glds instructions per wave per slice
-  static_assert(NBOX == 1 || WPIECES % WPT == 0, "every wave issues the same slice pieces");
-  uint16_t* const wring = smem + NBOX * HB * HALO;
-  uint16_t* const hbase = smem + box * HB * HALO;  // this box's halo buffer(s)
+  constexpr int WPW = (WPIECES + 255) / 256;  // glds instructions per wave per slice
+  uint16_t* const wring = smem + HB * HALO;
+  uint16_t* const hbase = smem;  // the halo buffer(s)
   auto issue_w = [&](int slot, const uint16_t* src) {
 #pragma unroll
     for (int i = 0; i < WPW; ++i) {
-      const int pb = i * WPT + wave_g * 64;
-      if (WPIECES % WPT == 0 || pb < WPIECES) glds16(src + (size_t)(pb + lane) * 8, wring + slot * WSL + pb * 8);
+      const int pb = i * 256 + wave * 64;
+      if (WPIECES % 256 == 0 || pb < WPIECES) glds16(src + (size_t)(pb + lane) * 8, wring + slot * WSL + pb * 8);
     }
   };
 
@@ -307,7 +306,8 @@ __global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_
 #pragma unroll
       for (int rt = 0; rt < RTW; ++rt) {
 #pragma unroll
-        for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
+        for (int ct = 0; ct < CTW; ++ct)
+          acc[rt][ct] = TR ? T::mfma(bfr[ct], fa[rt], acc[rt][ct]) : T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
         // (HB = 1: the next chunk's tap-0 fragments are read once its halo is in)
         if (HB == 2 || t < 8) fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
         if (PB && rt == 0) {
@@ -359,11 +359,49 @@ __global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_
     step(std::integral_constant<int, 7>{});
     step(std::integral_constant<int, 8>{});
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy slices land before LDS is reused
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy slices land before LDS is reused / the wave ends
+  const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
+  const int oy0 = POOL ? y0 / 2 : y0, ox0 = POOL ? x0 / 2 : x0;
+  if constexpr (TR) {
+    // lane: pixel m = row-tile base + (lane & 15), channels 4 * (lane >> 4) + r of each column tile
+    const int cq = 4 * (lane >> 4);
+#pragma unroll
+    for (int rt = 0; rt < RTW; ++rt) {
+      const int m = (wm * RTW + rt) * 16 + (lane & 15);
+      int oy, ox;
+      bool st_ok;
+      if constexpr (POOL) {
+        const int w = m >> 2;  // window-major: the 4 lanes of a window are lane & ~3 .. | 3
+        oy = w / (TW / 2);
+        ox = w - oy * (TW / 2);
+        st_ok = (lane & 3) == 0 && m < NPIX;
+      } else {
+        box_pixel<TW>(m, oy, ox);
+        st_ok = m < NPIX;
+      }
+      uint16_t* dst = out + (((size_t)b * Ho + oy0 + oy) * Wo + ox0 + ox) * Cout + nb * BN + wn * CTW * 16 + cq;
+#pragma unroll
+      for (int ct = 0; ct < CTW; ++ct) {
+        const f32x4 bv = *(const f32x4*)(bias + nb * BN + (wn * CTW + ct) * 16 + cq);
+        f32x4 v = acc[rt][ct];
+        if constexpr (POOL) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = fmaxf(v[r], quad_perm_f32<0xB1>(v[r]));  // lanes ^ 1
+            v[r] = fmaxf(v[r], quad_perm_f32<0x4E>(v[r]));  // lanes ^ 2
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = do_relu ? relu(v[r] + bv[r]) : v[r] + bv[r];
+        if (st_ok) *(u16x4*)(dst + ct * 16) = T::pack4(v);
+      }
+    }
+    return;
+  }
   __syncthreads();
 
   // Epilogue: folded-BN bias + ReLU (+ 2x2 max) -> 16-bit -> LDS -> global.
-  uint16_t* ostg = smem + box * OSTGB;
+  uint16_t* ostg = smem;
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct) {
     const int nl = (wn * CTW + ct) * 16 + (lane & 15);
@@ -385,8 +423,6 @@ __global__ __launch_bounds__(256 * NBOX, OCC) void conv3x3_bn_relu(const uint16_
     }
   }
   __syncthreads();
-  const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
-  const int oy0 = POOL ? y0 / 2 : y0, ox0 = POOL ? x0 / 2 : x0;
   store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
 }
 
@@ -715,7 +751,10 @@ int conv_block_n(int H, int cout) {
     case 224: return cout == 32 ? 32 : 0;
     case 112: return cout % 64 == 0 ? 64 : 0;
     case 56: return cout % 128 == 0 ? 128 : (cout % 64 == 0 ? 64 : 0);
-    case 28: return cout % 256 == 0 ? 256 : (cout % 192 == 0 ? 192 : (cout % 128 == 0 ? 128 : 0));
+    case 28:
+      // (BN 128 for cout 256, i.e. 7 rounds of 512 workgroups instead of 3.5,
+      // measured 6-8 % slower: the halved A reuse costs more than the tail)
+      return cout % 256 == 0 ? 256 : (cout % 192 == 0 ? 192 : (cout % 128 == 0 ? 128 : 0));
     case 14: return cout % 128 == 0 ? 128 : (cout % 192 == 0 ? 192 : (cout % 64 == 0 ? 64 : 0));
     default: return 0;
   }
@@ -723,24 +762,34 @@ int conv_block_n(int H, int cout) {
 
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
 // spill with it; no model pools after such a layer)
-template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true,
-          int NBOX = 1>
+static int g_conv_tr = 0;  // A/B switch (fac_set_option "conv_tr"): the TR epilogue in conv3x3_bn_relu
+void set_conv_tr(int v) { g_conv_tr = v; }
+
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   const int nbox = B * (H / TH) * (H / TW);
-  if (nbox % NBOX) return hipErrorInvalidValue;
-  dim3 grid(nbox / NBOX, Cout / BN);
+  dim3 grid(nbox, Cout / BN);
+  const bool tr = g_conv_tr != 0;
   if constexpr (POOLED) {
     if (pool) {
-      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, NBOX>
-          <<<grid, 256 * NBOX, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+      if (tr)
+        conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, true>
+            <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+      else
+        conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
+            <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, NBOX>
-      <<<grid, 256 * NBOX, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  if (tr)
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, true>
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  else
+    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
 
@@ -750,13 +799,24 @@ static hipError_t launch_db(const uint16_t* in, const uint16_t* wpk, const float
                             int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if (pool)
-    conv3x3_db<T, TH, TW, BN, WM, WN, true, OCC><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+    conv3x3_db<T, TH, TW, BN, WM, WN, true, OCC>
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   else
-    conv3x3_db<T, TH, TW, BN, WM, WN, false, OCC><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+    conv3x3_db<T, TH, TW, BN, WM, WN, false, OCC>
+        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
 
-static int g_conv_db = 0;  // A/B switch (fac_set_option "conv_db"), bit k: resolution 56 / 28 / 14
+
+// conv3x3_db for the 28^2 tiles (fac_set_option "conv_db": 1 = on, the
+// default; 0 = conv3x3_bn_relu, for A/Bs).  Same box, bit-identical outputs
+// (tools/db_ab.py, round 4): conv10-13 101.7/178.2/177.2/163.2 ->
+// 91.1/164.8/165.6/153.4 us.  At 56^2 it was neutral (B shared by two waves
+// of the 2x2 grid doubles its L2 reads), at 14^2 slower (the 1x4 tile needs
+// ~280 VGPRs and spills; the 2x2 tile pads 196 pixels to 224 rows), at
+// 112^2 15-20 % slower (four waves re-read the same B): those keep the LDS
+// weight ring.
+static int g_conv_db = 1;
 void set_conv_db(int v) { g_conv_db = v; }
 
 template <class T>
@@ -766,16 +826,9 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
   if (W != H) return hipErrorInvalidValue;
   if (g_conv_db) {
     switch (H * 1000 + conv_block_n(H, Cout)) {
-      case 56128:
-        if (g_conv_db & 1) return launch_db<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-        break;
-      case 28256:
-        if (g_conv_db & 2) return launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-        break;
-      case 14128:
-        if (g_conv_db & 8) return launch_db<T, 14, 14, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-        if (g_conv_db & 4) return launch_db<T, 14, 14, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-        break;
+      case 28256: return launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      case 28192: return launch_db<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      case 28128: return launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       default: break;
     }
   }

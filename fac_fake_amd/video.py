@@ -121,16 +121,19 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
     """Video probability (< 0.5 REAL, >= 0.5 FAKE) of one video.
 
     ``model``: fac_fake_amd.cvit.CViT (weights loaded, on this rank's GPU);
-    ``frames``: this rank's copy of the decoded video (device); ``boxes``:
-    [n, 5] (frame, left, top, right, bottom).  In dense mode with a process
-    group, every rank must call this with the same ``boxes``.
+    ``frames``: the decoded video, a device tensor or (dense mode) a host
+    array / CPU tensor, of which each rank then uploads only the frames of
+    its own shard of crops; ``boxes``: [n, 5] (frame, left, top, right,
+    bottom).  In dense mode with a process group, every rank must call this
+    with the same ``boxes``.
     """
-    length = int(frames.shape[0])
     if mode == "reference":
-        sel = reference_boxes(boxes, length)
+        fr, sel = select_reference(frames, boxes)
         if len(sel) == 0:
             return (float(EMPTY_SCORE), None) if return_logits else float(EMPTY_SCORE)
-        crops = crop_faces(frames, sel)
+        if not (isinstance(fr, torch.Tensor) and fr.is_cuda):
+            fr = torch.as_tensor(np.ascontiguousarray(fr)).to(torch.device("cuda", torch.cuda.current_device()))
+        crops = crop_faces(fr, sel)
         with torch.no_grad():
             logits = model.forward_u8(crops, pos_index=torch.from_numpy(chunk_slots(len(sel))))
     elif mode == "dense":
@@ -141,8 +144,19 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         world = dist.get_world_size(group) if group is not None or dist.is_initialized() else 1
         rank = dist.get_rank(group) if world > 1 else 0
         lo, hi = shard_bounds(n, world, rank)
+        dev = frames.device if isinstance(frames, torch.Tensor) and frames.is_cuda else \
+            torch.device("cuda", torch.cuda.current_device())
         if hi > lo:
-            crops = crop_faces(frames, boxes[lo:hi])
+            fr, sel = frames, boxes[lo:hi]
+            if not (isinstance(frames, torch.Tensor) and frames.is_cuda):
+                # a host video: this rank uploads only the frames of its own
+                # crops (a contiguous shard), not the whole decoded video
+                ids, inv = np.unique(sel[:, 0], return_inverse=True)
+                fr = torch.as_tensor(np.ascontiguousarray(np.asarray(frames)[ids.astype(np.int64)]))
+                fr = fr.to(torch.device("cuda", torch.cuda.current_device()))
+                sel = sel.copy()
+                sel[:, 0] = inv.reshape(-1).astype(np.int32)
+            crops = crop_faces(fr, sel)
             # one forward over the rank's crops: splitting them into pipelined
             # chunks (CViT.forward_u8_pipelined) measured slower for a 300-crop
             # video (4.73-5.13 vs 4.55 ms: two half batches fill the GPU worse
@@ -150,7 +164,7 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
             with torch.no_grad():
                 local = model.forward_u8(crops, pos_index=torch.from_numpy(dense_slots(hi - lo, offset=lo)))
         else:
-            local = torch.zeros(0, 2, dtype=torch.float32, device=frames.device)
+            local = torch.zeros(0, 2, dtype=torch.float32, device=dev)
         logits = gather_logits(local.float(), n, group) if world > 1 else local
     else:
         raise ValueError("mode must be 'reference' or 'dense'")
@@ -240,6 +254,8 @@ def segmented_video_scores(logits: torch.Tensor, seg) -> list:
     nv = len(seg) - 1
     if nv <= 0:
         return []
+    if int(seg[-1]) == 0:   # no crop in any of these videos: each scores 0.5 (cvit_prediction.py:218-219)
+        return [float(EMPTY_SCORE)] * nv
     logits = logits.float().contiguous()
     d_seg = torch.from_numpy(seg).to(logits.device)
     out = torch.empty(nv, dtype=torch.float32, device=logits.device)

@@ -190,7 +190,10 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * schedule, the default), "stem_nwg" (persistent fused-stem workgroups; 0 = one per
  * CU, the default), "ffn_ln_eps_exp" (n:
  * the FeedForward PreNorm LayerNorm uses eps = 10^-n; default 5, the RepBn8
- * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48). */
+ * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48), "conv_db" (1 = the
+ * 28x28 3x3 convs fetch their weight fragments straight into registers,
+ * conv3x3_db, the default; 0 = through the LDS weight ring; bit-identical
+ * outputs; process-wide, for A/B measurements). */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);

@@ -10,7 +10,8 @@
 * ResVitKan forward vs the reference module's logits (golden, fp32):
   per-logit sigmoid within 1e-3 with fp16 operands and, with bf16, within
   1.25x the oracle's emulated bf16 envelope on the same inputs (1.9e-3 for
-  ResVitKan, 0.8-1.0e-3 for S3D: tests/golden/bf16_envelope.json).
+  ResVitKan, 0.8-1.0e-3 for S3D: tests/golden/bf16_envelope.json) plus 5e-4
+  for the fp32 summation order (conftest.bf16_gate).
 """
 import numpy as np
 import pytest
@@ -414,6 +415,27 @@ def test_s3d_matches_reference(s3d_models, golden, srm, dt, tol16):
     p_ref = 1 / (1 + np.exp(-g[f"logits_{srm}"].astype(np.float64)))
     assert lg.shape == (2, 1)
     assert np.abs(pr.cpu().numpy() - p_ref).max() <= tol
+
+
+@pytest.mark.parametrize("srm", ["no", "yes"])
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_s3d_reference_harness_shape(s3d_models, golden, srm, dt):
+    """The reference harness's clip shape (S3D-test.py:130-190: 200 frames,
+    every 10th kept -> 20; model.py:344-354 profiles 20 x 224 x 224): 2 raw
+    content-varied clips through the drop-in vs the reference module
+    (tests/golden/s3d_golden_20x224.npz).  fp16 within the 1e-3 bar, bf16
+    within 1.25x the oracle's emulated bf16 envelope at this shape (plus
+    the accumulation-order allowance, conftest.ORDER_NOISE)."""
+    from fac_fake_amd.weights import s3d_clips_varied
+    g = golden("s3d_golden_20x224.npz")
+    x = torch.from_numpy(s3d_clips_varied(2, int(g["frames"]), int(g["size"]), seed=int(g["clip_seed"]))).to(DEV)
+    lg, pr = s3d_models[(srm, dt)](x, return_probs=True)
+    torch.cuda.synchronize()
+    p_ref = 1 / (1 + np.exp(-g[f"logits_{srm}"].astype(np.float64)))
+    from conftest import bf16_gate
+    tol = 1e-3 if dt == "fp16" else bf16_gate(float(g[f"env_prob_{srm}_bf16"]))
+    assert lg.shape == (2, 1)
+    assert np.abs(pr.cpu().numpy() - p_ref).max() <= tol, (np.abs(pr.cpu().numpy() - p_ref).max(), tol)
 
 
 def _rel_to_rms(got, ref):

@@ -6,8 +6,9 @@ Tolerances (stated per test):
 * bf16 operands: exact bf16 rounding of the operands alone already moves the
   fp32 reference by 1.5e-3 .. 5.3e-3 in probability on these fixtures (the
   oracle's emulation, tests/golden/bf16_envelope.json), so
-  end-to-end bf16 is gated at 1.25x that envelope per fixture (conftest
-  tol16), and the kernels themselves are gated
+  end-to-end bf16 is gated at 1.25x that envelope per fixture plus 5e-4
+  for the HIP path's fp32 summation order (conftest tol16 / bf16_gate), and
+  the kernels themselves are gated
   tightly per kernel: each conv fed the oracle's previous-layer output agrees
   to <= 2 ulp (1-ulp accumulation-order flips on a few % of outputs), the
   tail fed the oracle's stem output agrees within 1e-3 in probability, and
@@ -557,6 +558,62 @@ def test_multi_video_batching_matches_per_video(models):
         got, lg = predict_videos(m, src, batch=batch, device=DEV, return_logits=True)
         assert got == list(want), (batch, got, want)
         assert torch.equal(lg.cpu(), ref_lg), batch
+
+
+@pytest.mark.parametrize("mode", ["reference", "dense"])
+def test_host_frames_upload_only_what_is_cropped(models, mode):
+    """A host video (numpy) gives the same score and logits as the same
+    video resident on the device: predict_video then uploads only the frames
+    its (this rank's) crops come from."""
+    from fac_fake_amd.video import predict_video, synthetic_video
+    m = models["bf16"]
+    frames, boxes = synthetic_video(120, 360, 640, seed=21, device=DEV, faces_per_frame=2)
+    s_dev, lg_dev = predict_video(m, frames, boxes, mode=mode, return_logits=True)
+    s_host, lg_host = predict_video(m, frames.cpu().numpy(), boxes, mode=mode, return_logits=True)
+    assert s_dev == s_host and torch.equal(lg_dev.cpu(), lg_host.cpu())
+
+
+@pytest.mark.parametrize("cin,cout,pool", [(128, 256, 0), (256, 256, 1), (96, 192, 0), (160, 128, 1), (32, 128, 0)])
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+def test_conv_db_tile_equals_weight_ring(models, cin, cout, pool, dt):
+    """The 28x28 3x3 convs default to conv3x3_db (weight fragments straight
+    into registers, register-staged halo, one barrier per 32-channel chunk).
+    Same k order and MFMA sequence as conv3x3_bn_relu (LDS weight ring), so
+    the outputs are bit-identical, for every 28^2 column tile (BN 256 / 192 /
+    128: CViT, S3D, ResNet), odd and even chunk counts, a single chunk,
+    ragged batch, and with the fused 2x2 max-pool."""
+    from fac_fake_amd import _lib
+    from fac_fake_amd.ops import TORCH16, _zero256
+    lib = _lib.load()
+    m = models[dt]
+    g = torch.Generator().manual_seed(cin + cout + pool)
+    n = 5
+    x = torch.randn(n, 28, 28, cin, generator=g).relu().to(TORCH16[dt]).to(DEV)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(9 * cin)).contiguous()
+    b = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    ne = lib.fac_conv3x3_packed_elems(28, cin, cout)
+    pk = torch.empty(ne, dtype=torch.int16)
+    _lib.check(lib.fac_conv3x3_pack(_lib.DTYPES[dt], 28, cin, cout, w.data_ptr(), pk.data_ptr()), None, "pack")
+    pk = pk.to(DEV)
+    ho = 14 if pool else 28
+    outs = []
+    for db in (1, 0):
+        m.set_option("conv_db", db)
+        y = torch.empty(n, ho, ho, cout, dtype=TORCH16[dt], device=DEV)
+        _lib.check(lib.fac_conv3x3(_lib.DTYPES[dt], x.data_ptr(), pk.data_ptr(), b.data_ptr(), y.data_ptr(), n, 28,
+                                   cin, cout, pool, 1, _zero256(x.device).data_ptr(),
+                                   torch.cuda.current_stream().cuda_stream), None, "fac_conv3x3")
+        outs.append(y)
+    m.set_option("conv_db", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    ref = torch.nn.functional.conv2d(x.cpu().float().permute(0, 3, 1, 2), w.to(TORCH16[dt]).float(), b.cpu(),
+                                     padding=1).relu()
+    if pool:
+        ref = torch.nn.functional.max_pool2d(ref, 2)
+    ref = ref.permute(0, 2, 3, 1)
+    got = outs[0].cpu().float()
+    assert torch.allclose(got, ref, rtol=2 * ULP_REL[dt], atol=1e-2), float((got - ref).abs().max())
 
 
 def test_stem_event_timing(models):

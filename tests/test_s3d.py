@@ -35,6 +35,17 @@ def test_oracle_matches_reference_goldens(golden, torch_threads, srm):
 
 
 @pytest.mark.parametrize("srm", ["no", "yes"])
+def test_oracle_matches_reference_at_harness_shape(golden, torch_threads, srm):
+    """20 x 224 x 224 clips (S3D-test.py:130-190, model.py:344-354)."""
+    from fac_fake_amd.weights import s3d_clips_varied
+    from oracle import s3d_torch as O
+    g = golden("s3d_golden_20x224.npz")
+    x = torch.from_numpy(s3d_clips_varied(2, int(g["frames"]), int(g["size"]), seed=int(g["clip_seed"])))
+    out = O.forward_fp32(make_s3d_state_dict(0, 1, srm == "yes"), x, srm == "yes").numpy()
+    assert np.abs(out - g[f"logits_{srm}"]).max() <= 1e-5
+
+
+@pytest.mark.parametrize("srm", ["no", "yes"])
 def test_emulation_within_16bit_envelope(golden, torch_threads, srm):
     from oracle import s3d_torch as O
     g = golden("s3d_golden.npz")

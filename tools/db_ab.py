@@ -28,14 +28,28 @@ def main():
     ap.add_argument("--arms", default="0,7")
     ap.add_argument("--key", default="conv_db")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--pre", action="append", default=[], metavar="KEY=VALUE",
+                    help="process-wide fac_set_option applied once before the arms (e.g. conv28_lds=32768)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    m = CViT(dtype=args.dtype)
-    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_state_dict(0).items()})
-    m.to(dev)
-    m.reserve(8, dev)
-    lib = _lib.load()
     arms = [int(a) for a in args.arms.split(",")]
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in make_state_dict(0).items()}
+    # options that change the weight packing (conv28_bn) need one model per
+    # arm, packed while that arm's value is set; the others share one model
+    models = {}
+    for a in (arms if args.key == "conv28_bn" else arms[:1]):
+        m = CViT(dtype=args.dtype)
+        m.load_state_dict(sd)
+        m.to(dev)
+        if models:
+            next(iter(models.values())).set_option(args.key, a)
+        m.reserve(8, dev)
+        models[a] = m
+    model_of = (lambda a: models[a]) if args.key == "conv28_bn" else (lambda a: models[arms[0]])
+    for kv in args.pre:
+        k, v = kv.split("=")
+        model_of(arms[0]).set_option(k, int(v))
+    lib = _lib.load()
     B = args.B
     res = {}
     tot = {a: 0.0 for a in arms}
@@ -48,10 +62,11 @@ def main():
         s = torch.cuda.Stream()
         outs, graphs = {}, {}
         for a in arms:
+            m = model_of(a)
             m.set_option(args.key, a)
             y = torch.empty(B, Ho, Ho, Cout, dtype=x.dtype, device=dev)
 
-            def call(y=y):
+            def call(y=y, m=m):
                 _lib.check(lib.fac_debug_conv(m._ctx, layer, x.data_ptr(), B, y.data_ptr(),
                                               torch.cuda.current_stream().cuda_stream), m._ctx, "debug_conv")
             with torch.cuda.stream(s):
@@ -70,6 +85,7 @@ def main():
         times = {a: [] for a in arms}
         for _ in range(args.reps):
             for a in arms:
+                model_of(a).set_option(args.key, a)
                 graphs[a].replay()
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -88,7 +104,7 @@ def main():
                       "ndiff": ndiff[a]}
         res[f"conv{layer + 1}"] = row
         print(json.dumps({f"conv{layer + 1}": row}), flush=True)
-    m.set_option(args.key, arms[0])
+    model_of(arms[0]).set_option(args.key, arms[0])
     print(json.dumps({"dtype": args.dtype, "total_us": {a: round(t, 1) for a, t in tot.items()}}), flush=True)
 
 

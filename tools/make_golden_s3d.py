@@ -102,5 +102,34 @@ def blocks(S3D):
     np.savez_compressed(OUT / "s3d_golden_blocks.npz", **out)
 
 
+def harness_shape(S3D):
+    """The reference harness's clip shape (S3D-test.py:130-190 reads 200
+    frames and keeps every 10th: 20 frames; model.py:344-354 profiles
+    20 x 224 x 224): 2 raw clips of 20 x 224 x 224 (s3d_clips_varied, seed 37)
+    through S3D(1, 'no') and S3D(1, 'yes') -> s3d_golden_20x224.npz (logits,
+    plus each variant's emulated 16-bit rounding envelope in probability)."""
+    from oracle import s3d_torch as O
+    x = torch.from_numpy(s3d_clips_varied(2, 20, 224, seed=37))
+    out = {"clip_seed": np.int64(37), "frames": np.int64(20), "size": np.int64(224)}
+    for srm in ("no", "yes"):
+        m = S3D(1, srm).eval()
+        sd = make_s3d_state_dict(0, 1, srm == "yes")
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        with torch.no_grad():
+            lg = m(x).numpy()
+        out[f"logits_{srm}"] = lg
+        p_ref = 1 / (1 + np.exp(-lg.astype(np.float64)))
+        for dt in ("fp16", "bf16"):
+            pe = torch.sigmoid(O.forward_emulated(sd, x, srm == "yes", dt)).double().numpy()
+            out[f"env_prob_{srm}_{dt}"] = np.float64(np.abs(pe - p_ref).max())
+        print(srm, "20x224 probs", np.round(p_ref.ravel(), 5), out[f"env_prob_{srm}_fp16"], out[f"env_prob_{srm}_bf16"])
+    np.savez_compressed(OUT / "s3d_golden_20x224.npz", **out)
+
+
 if __name__ == "__main__":
-    main()
+    if "--harness-shape" in sys.argv:
+        sys.path.insert(0, str(REF))
+        from model import S3D as _S3D  # the reference module
+        harness_shape(_S3D)
+    else:
+        main()
