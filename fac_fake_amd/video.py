@@ -132,7 +132,7 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         if len(sel) == 0:
             return (float(EMPTY_SCORE), None) if return_logits else float(EMPTY_SCORE)
         if not (isinstance(fr, torch.Tensor) and fr.is_cuda):
-            fr = torch.as_tensor(np.ascontiguousarray(fr)).to(torch.device("cuda", torch.cuda.current_device()))
+            fr = torch.as_tensor(np.ascontiguousarray(fr)).to(_work_device(frames))
         crops = crop_faces(fr, sel)
         with torch.no_grad():
             logits = model.forward_u8(crops, pos_index=torch.from_numpy(chunk_slots(len(sel))))
@@ -144,16 +144,14 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         world = dist.get_world_size(group) if group is not None or dist.is_initialized() else 1
         rank = dist.get_rank(group) if world > 1 else 0
         lo, hi = shard_bounds(n, world, rank)
-        dev = frames.device if isinstance(frames, torch.Tensor) and frames.is_cuda else \
-            torch.device("cuda", torch.cuda.current_device())
+        dev = _work_device(frames)
         if hi > lo:
             fr, sel = frames, boxes[lo:hi]
             if not (isinstance(frames, torch.Tensor) and frames.is_cuda):
                 # a host video: this rank uploads only the frames of its own
                 # crops (a contiguous shard), not the whole decoded video
                 ids, inv = np.unique(sel[:, 0], return_inverse=True)
-                fr = torch.as_tensor(np.ascontiguousarray(np.asarray(frames)[ids.astype(np.int64)]))
-                fr = fr.to(torch.device("cuda", torch.cuda.current_device()))
+                fr = torch.as_tensor(np.ascontiguousarray(np.asarray(frames)[ids.astype(np.int64)])).to(dev)
                 sel = sel.copy()
                 sel[:, 0] = inv.reshape(-1).astype(np.int32)
             crops = crop_faces(fr, sel)
@@ -170,6 +168,15 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         raise ValueError("mode must be 'reference' or 'dense'")
     score = device_video_score(logits)
     return (score, logits) if return_logits else score
+
+
+def _work_device(frames) -> torch.device:
+    """Where a video's crops are made: the frames' GPU, else the current GPU
+    (host frames are uploaded there); a CPU-only process keeps host frames on
+    the CPU (the model call then fails loudly: there is no CPU path)."""
+    if isinstance(frames, torch.Tensor) and frames.is_cuda:
+        return frames.device
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
 
 
 def select_reference(frames, boxes):
