@@ -41,12 +41,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                    (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
-// value of lane (quad_perm CTRL) within each group of 4 lanes (DPP, no LDS)
-template <int CTRL>
-__device__ __forceinline__ float quad_perm_f32(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
-
 template <int TW>
 constexpr int halo_rp() { return TW + 2 <= 24 ? 24 : 40; }
 
@@ -86,13 +80,7 @@ __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, 
 // 1: it is loaded between chunks, exposed, which halves the halo LDS so that
 // OCC = 3 workgroups share a CU and hide each other's exposed loads — the
 // 112^2 layers, whose 1-2 chunks leave little to pipeline within a box).
-// TR: transposed MFMA (D^T = W . A^T: weights as the A operand, pixels as B),
-// so each lane holds 4 consecutive output channels of one pixel and the
-// epilogue stores them straight to NHWC global memory (8 bytes per lane, the
-// 2x2 max-pool across the 4 lanes of a window by DPP) instead of 2-byte LDS
-// staging writes, a barrier and a raster copy.
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
-          bool TR = false>
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true>
 __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
@@ -306,8 +294,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
 #pragma unroll
       for (int rt = 0; rt < RTW; ++rt) {
 #pragma unroll
-        for (int ct = 0; ct < CTW; ++ct)
-          acc[rt][ct] = TR ? T::mfma(bfr[ct], fa[rt], acc[rt][ct]) : T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
+        for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
         // (HB = 1: the next chunk's tap-0 fragments are read once its halo is in)
         if (HB == 2 || t < 8) fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
         if (PB && rt == 0) {
@@ -362,45 +349,15 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy slices land before LDS is reused / the wave ends
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const int oy0 = POOL ? y0 / 2 : y0, ox0 = POOL ? x0 / 2 : x0;
-  if constexpr (TR) {
-    // lane: pixel m = row-tile base + (lane & 15), channels 4 * (lane >> 4) + r of each column tile
-    const int cq = 4 * (lane >> 4);
-#pragma unroll
-    for (int rt = 0; rt < RTW; ++rt) {
-      const int m = (wm * RTW + rt) * 16 + (lane & 15);
-      int oy, ox;
-      bool st_ok;
-      if constexpr (POOL) {
-        const int w = m >> 2;  // window-major: the 4 lanes of a window are lane & ~3 .. | 3
-        oy = w / (TW / 2);
-        ox = w - oy * (TW / 2);
-        st_ok = (lane & 3) == 0 && m < NPIX;
-      } else {
-        box_pixel<TW>(m, oy, ox);
-        st_ok = m < NPIX;
-      }
-      uint16_t* dst = out + (((size_t)b * Ho + oy0 + oy) * Wo + ox0 + ox) * Cout + nb * BN + wn * CTW * 16 + cq;
-#pragma unroll
-      for (int ct = 0; ct < CTW; ++ct) {
-        const f32x4 bv = *(const f32x4*)(bias + nb * BN + (wn * CTW + ct) * 16 + cq);
-        f32x4 v = acc[rt][ct];
-        if constexpr (POOL) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = fmaxf(v[r], quad_perm_f32<0xB1>(v[r]));  // lanes ^ 1
-            v[r] = fmaxf(v[r], quad_perm_f32<0x4E>(v[r]));  // lanes ^ 2
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = do_relu ? relu(v[r] + bv[r]) : v[r] + bv[r];
-        if (st_ok) *(u16x4*)(dst + ct * 16) = T::pack4(v);
-      }
-    }
-    return;
-  }
   __syncthreads();
 
   // Epilogue: folded-BN bias + ReLU (+ 2x2 max) -> 16-bit -> LDS -> global.
+  // (Round 4, measured and not kept: the transposed MFMA, D^T = W . A^T, so
+  // that each lane holds 4 channels of one pixel and stores them straight to
+  // global memory as 8 bytes, the 2x2 max by DPP across a window's 4 lanes.
+  // Bit-identical outputs, but 2-23 % slower on every tile, conv4 165 -> 195
+  // and conv6 203 -> 249 us: 16 8-byte stores of 32-byte segments per wave
+  // against 8 fully coalesced 16-byte ones after the LDS transpose.)
   uint16_t* ostg = smem;
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct) {
@@ -762,34 +719,22 @@ int conv_block_n(int H, int cout) {
 
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
 // spill with it; no model pools after such a layer)
-static int g_conv_tr = 0;  // A/B switch (fac_set_option "conv_tr"): the TR epilogue in conv3x3_bn_relu
-void set_conv_tr(int v) { g_conv_tr = v; }
-
 template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   const int nbox = B * (H / TH) * (H / TW);
   dim3 grid(nbox, Cout / BN);
-  const bool tr = g_conv_tr != 0;
   if constexpr (POOLED) {
     if (pool) {
-      if (tr)
-        conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, true>
-            <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
-      else
-        conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
-            <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
+          <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  if (tr)
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, true>
-        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
-  else
-    conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
-        <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
+      <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
 

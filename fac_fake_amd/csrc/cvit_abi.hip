@@ -23,7 +23,6 @@
 namespace fac {
 int conv_block_n(int H, int cout);
 void set_conv_db(int v);
-void set_conv_tr(int v);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
@@ -725,10 +724,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   }
   if (k == "conv_db") {  // 1 (default): conv3x3_db for the 28^2 tiles; 0: the LDS weight ring (A/B); process-wide
     fac::set_conv_db(value);
-    return FAC_OK;
-  }
-  if (k == "conv_tr") {  // A/B, process-wide: transposed-MFMA direct-store epilogue of conv3x3_bn_relu
-    fac::set_conv_tr(value);
     return FAC_OK;
   }
   if (k == "stem_dynamic") {
