@@ -44,6 +44,14 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
 template <int TW>
 constexpr int halo_rp() { return TW + 2 <= 24 ? 24 : 40; }
 
+// Each box shape serves exactly one image size (launch_conv_t picks the tile
+// by resolution): make it a compile-time constant inside the kernels, so the
+// box-index divisions and the halo map's address arithmetic fold.
+template <int TH, int TW, int BN>
+constexpr int tile_res() {
+  return TW == 16 ? (BN == 32 ? 224 : 112) : (TH == 8 ? 56 : (TH == 4 ? 28 : (TH == 14 ? 14 : 0)));
+}
+
 template <int TW>
 __device__ __forceinline__ void box_pixel(int m, int& py, int& px) {
   constexpr int WW = TW / 2;
@@ -126,6 +134,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   static_assert(CTW * 16 * WN == BN, "BN split");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
+  static_assert(tile_res<TH, TW, BN>() > 0, "tile shape without a resolution");
+  H = W = tile_res<TH, TW, BN>();  // == the launch's H (launch_conv_t); folds the index math
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
@@ -432,6 +442,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restric
   static_assert(CTW * 16 * WN == BN, "BN split");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
+  static_assert(tile_res<TH, TW, BN>() > 0, "tile shape without a resolution");
+  H = W = tile_res<TH, TW, BN>();  // == the launch's H (launch_conv_t); folds the index math
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;

@@ -33,7 +33,7 @@ hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uin
                        void* out, int ldo, int M, int N, int K, int splits, hipStream_t st, int variant = -1);
 hipError_t launch_embed_finalize_ln(int dtype, const float* slab, int S, int B, const float* bias, const float* cls,
                                     const float* pos, const int32_t* pidx, float* x, const float* g, const float* bt,
-                                    uint16_t* y, int* err, hipStream_t st);
+                                    uint16_t* y, int* err, int seq, hipStream_t st);
 hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,
                             hipStream_t st);
 hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipStream_t st);
@@ -138,6 +138,7 @@ struct fac_ctx {
   // host at the start of the next forward without a device sync
   int* errflag = nullptr;      // device view
   int* err_host = nullptr;     // host view of the same int
+  int fwd_seq = 0;             // forwards on this context (the flag holds the offending one's number)
   int* sched = nullptr;  // 2 ints: stem224 dynamic box counter + finished-workgroup count
   int stem_dynamic = 0;  // option "stem_dynamic": stem224 claims boxes from `sched` (default: static, no atomics)
   int stem_nwg = 0;      // option "stem_nwg": persistent stem workgroups (0 = one per CU)
@@ -169,8 +170,12 @@ int set_err(fac_ctx* c, int code, const std::string& msg) {
 // on the host, at the next call — no synchronisation)
 int take_device_error(fac_ctx* c) {
   if (c && c->err_host && *(volatile int*)c->err_host) {
+    const int bad = *(volatile int*)c->err_host;
     *(volatile int*)c->err_host = 0;
-    return set_err(c, FAC_ERR_ARG, "a previous forward had a pos_index outside [0,32) (clamped on the device)");
+    return set_err(c, FAC_ERR_ARG, "forward call #" + std::to_string(bad) + " of this context (this call is #" +
+                                       std::to_string(c->fwd_seq + 1) +
+                                       ") had a pos_index outside [0,32), clamped on the device; this call was "
+                                       "not run");
   }
   return 0;
 }
@@ -617,7 +622,7 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
                          kPatchDim, S, st, c->gemm_var[0]));
   // residual stream rows + layer 0's PreNorm LayerNorm in one pass
   HIP_TRY(c, launch_embed_finalize_ln(dt, c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->tl[0].ln1_g,
-                                      c->tl[0].ln1_b, c->xn, c->errflag, st));
+                                      c->tl[0].ln1_b, c->xn, c->errflag, ++c->fwd_seq, st));
   MARK(17);
   const int R = 2 * B;
   const float scale = 1.0f / std::sqrt((float)kDim);  // dim ** -0.5 (cvit.py:38), not head_dim

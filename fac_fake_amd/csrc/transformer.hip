@@ -201,11 +201,12 @@ __global__ __launch_bounds__(64) void embed_finalize_ln(const float* __restrict_
                                                         const float* __restrict__ pos,
                                                         const int32_t* __restrict__ pidx, float* __restrict__ x,
                                                         const float* __restrict__ g, const float* __restrict__ bta,
-                                                        uint16_t* __restrict__ y, int* __restrict__ err) {
+                                                        uint16_t* __restrict__ y, int* __restrict__ err, int seq) {
   const int r = blockIdx.x, b = r >> 1, lane = threadIdx.x;
   int p = pidx[b];
   if (p < 0 || p >= 32) {
-    if (lane == 0 && (r & 1) == 0 && err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the flag names the forward (its call number on the context, >= 1)
+    if (lane == 0 && (r & 1) == 0 && err) __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     p = p < 0 ? 0 : 31;
   }
   f32x4 v[4];
@@ -482,11 +483,11 @@ hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uin
 template <class T>
 static hipError_t embed_ln_t(const float* slab, int S, int B, const float* bias, const float* cls, const float* pos,
                              const int32_t* pidx, float* x, const float* g, const float* bt, uint16_t* y, int* err,
-                             hipStream_t st) {
+                             int seq, hipStream_t st) {
   switch (S) {
-    case 7: embed_finalize_ln<T, 7><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err); break;
-    case 14: embed_finalize_ln<T, 14><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err); break;
-    case 28: embed_finalize_ln<T, 28><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err); break;
+    case 7: embed_finalize_ln<T, 7><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err, seq); break;
+    case 14: embed_finalize_ln<T, 14><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err, seq); break;
+    case 28: embed_finalize_ln<T, 28><<<2 * B, 64, 0, st>>>(slab, B, bias, cls, pos, pidx, x, g, bt, y, err, seq); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -494,9 +495,9 @@ static hipError_t embed_ln_t(const float* slab, int S, int B, const float* bias,
 
 hipError_t launch_embed_finalize_ln(int dtype, const float* slab, int S, int B, const float* bias, const float* cls,
                                     const float* pos, const int32_t* pidx, float* x, const float* g, const float* bt,
-                                    uint16_t* y, int* err, hipStream_t st) {
-  if (dtype == 0) return embed_ln_t<BF16>(slab, S, B, bias, cls, pos, pidx, x, g, bt, y, err, st);
-  return embed_ln_t<F16>(slab, S, B, bias, cls, pos, pidx, x, g, bt, y, err, st);
+                                    uint16_t* y, int* err, int seq, hipStream_t st) {
+  if (dtype == 0) return embed_ln_t<BF16>(slab, S, B, bias, cls, pos, pidx, x, g, bt, y, err, seq, st);
+  return embed_ln_t<F16>(slab, S, B, bias, cls, pos, pidx, x, g, bt, y, err, seq, st);
 }
 
 hipError_t launch_layernorm(int dtype, const float* x, const float* g, const float* b, uint16_t* y, int R,

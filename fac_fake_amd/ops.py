@@ -148,11 +148,10 @@ class ConvLayer:
             self._pk33 = {}
             self._device = device
             _zero256(torch.device(device))  # allocated (and zeroed) before any graph capture
-            # packed now for every resolution conv.hip has tiles for, so a
-            # forward never packs (a synchronous host->device copy) inside a
-            # graph capture
-            for h in (112, 56, 28, 14, 7):
-                self._packed33(h)
+            # conv.hip weights are packed on first use per input size (a
+            # synchronous host->device copy: run one eager forward before
+            # graph capture, which every caller here does), so a layer holds
+            # only the packings of the sizes it sees
 
     def _packed33(self, h: int):
         """fac_conv3x3 weights for h x h inputs, or None if conv.hip has no tile for it."""

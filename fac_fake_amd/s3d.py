@@ -158,18 +158,26 @@ class S3D(nn.Module):
                 # (3,1,1) halves take the uniform-tap gather too
                 m1 = (b1b + 63) // 64 * 64 if self.padt else b1b
                 m2 = (b2b + 63) // 64 * 64 if self.padt else b2b
-                merged_p = merged
-                if (p1, p2) != (b1a, b2a):
-                    hw = [heads[0][0], _pad_rows(heads[1][0], p1), _pad_rows(heads[2][0], p2)]
-                    hb = [heads[0][1], _pad_rows(heads[1][1], p1), _pad_rows(heads[2][1], p2)]
-                    merged_p = ConvLayer(torch.cat(hw), torch.cat(hb), 1, 0, dtype=dt, device=device)
                 b1, b2 = sep(f"{p}.branch1.1", 3, 1, 1), sep(f"{p}.branch2.1", 3, 1, 1)
+
+                def padded(p=p, heads=heads, merged=merged, b1=b1, b2=b2, b1a=b1a, b1b=b1b, b2a=b2a, b2b=b2b,
+                           p1=p1, p2=p2, m1=m1, m2=m2):
+                    # the channel-padded layers, built on the block's first
+                    # forward below 14x14 (never for the larger
+                    # blocks, whose padded copies no launch reads)
+                    merged_p = merged
+                    if (p1, p2) != (b1a, b2a):
+                        hw = [heads[0][0], _pad_rows(heads[1][0], p1), _pad_rows(heads[2][0], p2)]
+                        hb = [heads[0][1], _pad_rows(heads[1][1], p1), _pad_rows(heads[2][1], p2)]
+                        merged_p = ConvLayer(torch.cat(hw), torch.cat(hb), 1, 0, dtype=dt, device=device)
+                    return dict(
+                        b1p=b1 if (p1, m1) == (b1a, b1b) else sep(f"{p}.branch1.1", 3, 1, 1, cin_pad=p1, mid_pad=m1),
+                        b2p=b2 if (p2, m2) == (b2a, b2b) else sep(f"{p}.branch2.1", 3, 1, 1, cin_pad=p2, mid_pad=m2),
+                        heads_p=merged_p)
                 self._layers.append(("mixed", dict(
-                    b1=b1, b2=b2, b3=bconv(f"{p}.branch3.1"),
-                    b1p=b1 if (p1, m1) == (b1a, b1b) else sep(f"{p}.branch1.1", 3, 1, 1, cin_pad=p1, mid_pad=m1),
-                    b2p=b2 if (p2, m2) == (b2a, b2b) else sep(f"{p}.branch2.1", 3, 1, 1, cin_pad=p2, mid_pad=m2),
+                    b1=b1, b2=b2, b3=bconv(f"{p}.branch3.1"), padded=padded,
                     heads=merged, head_splits=(b0, b0 + b1a), head_widths=(b1a, b2a),
-                    heads_p=merged_p, head_splits_p=(b0, b0 + p1), head_widths_p=(p1, p2),
+                    head_splits_p=(b0, b0 + p1), head_widths_p=(p1, p2),
                     widths=(b0, b1b, b2b, b3))))
         self._fc = ConvLayer(sd["fc.0.weight"], sd["fc.0.bias"], 1, 0, dtype=dt, device=device)
         self._prep = (idx, v)
@@ -203,6 +211,11 @@ class S3D(nn.Module):
         o2 = o1 + blk["widths"][1]
         o3 = o2 + blk["widths"][2]
         sfx = "_p" if h < 14 else ""   # channel-padded heads (pad64_level) where no conv.hip tile exists
+        if sfx and "heads_p" not in blk:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("S3D: run one eager forward at this clip size before graph capture "
+                                   "(the padded late-block layers are built on first use)")
+            blk.update(blk["padded"]())
         s1, t1 = blk["b1p" if sfx else "b1"]
         s2, t2 = blk["b2p" if sfx else "b2"]
         hws = blk["head_widths" + sfx]

@@ -146,9 +146,10 @@ int fac_stem_event_ms(fac_ctx* ctx, float* avg_ms, int* n_launches);
 /* pos_index outside [0,32): the device clamps it (the kernel cannot return
  * an error) and raises a host-visible flag; the context's NEXT forward call
  * (fac_forward_*, fac_forward_features, pipelined) then returns FAC_ERR_ARG
- * before enqueueing anything and clears the flag.  fac_check_device_errors
- * reads (and clears) the flag after synchronising the device: nonzero if a
- * forward since the last check saw such an index.  Not for use inside graph
+ * before enqueueing anything and clears the flag; fac_last_error names the
+ * offending forward by its call number on the context.  fac_check_device_errors
+ * reads (and clears) the flag after synchronising the device: 0, or the call
+ * number (>= 1) of a forward since the last check that saw such an index.  Not for use inside graph
  * capture (a captured forward's flag is seen by the first eager call after
  * the replay completes). */
 int fac_check_device_errors(fac_ctx* ctx, int* flags);

@@ -133,7 +133,7 @@ def test_bottleneck_pw2_matches_two_launches(cin, cmid, n1, hw, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
-@pytest.mark.parametrize("n,d,h,w", [(2, 1, 19, 59), (1, 2, 35, 31), (3, 1, 115, 115)])
+@pytest.mark.parametrize("n,d,h,w", [(2, 1, 19, 59), (1, 2, 35, 31), (3, 1, 115, 115), (300, 1, 19, 59)])
 def test_conv_s2d4_maxpool_fused(n, d, h, w, dt):
     """conv_s2d4_mp (FAC_CONV_MAXPOOL3S2): the 4x4/1 space-to-depth conv +
     bias + ReLU + MaxPool2d(3, 2, 1) in one launch is bit-identical to
@@ -141,7 +141,9 @@ def test_conv_s2d4_maxpool_fused(n, d, h, w, dt):
     rounding is monotone), and within one 16-bit ulp of torch's fp32 conv ->
     relu -> rounded -> max_pool.  Every box touches the top or left pool
     padding on the first row / column of boxes; biases straddle 0 so ReLU
-    zeros occur."""
+    zeros occur.  300 images of 2 column strips each (600 > 2 x 256 CUs):
+    each persistent workgroup walks several strips (the carry reset, the
+    cross-strip halo prefetch and its counted waits)."""
     from fac_fake_amd.ops import ConvLayer, max_pool_sep
     g = torch.Generator().manual_seed(7 + h + d)
     x = torch.randn(n, 16, d, h, w, generator=g).to(T16[dt]).float()

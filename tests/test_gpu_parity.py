@@ -302,11 +302,15 @@ def test_out_of_range_pos_index_is_an_error_at_the_c_abi(models):
     assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
     torch.cuda.synchronize()
     rc = lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st)
-    assert rc == -1 and b"pos_index" in lib.fac_last_error(ctx)
+    msg = lib.fac_last_error(ctx)
+    # the error names the offending forward: call #n, and this one #n+1
+    import re
+    got = re.search(rb"forward call #(\d+) of this context \(this call is #(\d+)\)", msg)
+    assert rc == -1 and b"pos_index" in msg and got and int(got.group(2)) == int(got.group(1)) + 1, msg
     assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0  # cleared
     assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
     flags = ctypes.c_int()
-    assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == 1
+    assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == int(got.group(1)) + 2
     assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == 0
     assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0
     torch.cuda.synchronize()
