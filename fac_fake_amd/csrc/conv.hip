@@ -724,6 +724,8 @@ int conv_block_n(int H, int cout) {
       // (BN 128 for cout 256, i.e. 7 rounds of 512 workgroups instead of 3.5,
       // measured 6-8 % slower: the halved A reuse costs more than the tail)
       return cout % 256 == 0 ? 256 : (cout % 192 == 0 ? 192 : (cout % 128 == 0 ? 128 : 0));
+    // (round 4: BN 256 as 1 x 4 waves of 208 x 64, half the A reads per MFMA,
+    // one workgroup per CU: conv14-17 613 -> 632 us, not kept)
     case 14: return cout % 128 == 0 ? 128 : (cout % 192 == 0 ? 192 : (cout % 64 == 0 ? 64 : 0));
     default: return 0;
   }

@@ -20,6 +20,9 @@ from fac_fake_amd.weights import make_state_dict  # noqa: E402
 from tools.conv_sweep import LAYERS  # noqa: E402
 
 
+PACKING_KEYS = ()   # options that change the weight packing (none left): one model per arm
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16")
@@ -34,10 +37,11 @@ def main():
     dev = torch.device("cuda:0")
     arms = [int(a) for a in args.arms.split(",")]
     sd = {k: torch.from_numpy(np.asarray(v)) for k, v in make_state_dict(0).items()}
-    # options that change the weight packing (conv28_bn) need one model per
-    # arm, packed while that arm's value is set; the others share one model
+    # options that change the weight packing need one model per arm, packed
+    # while that arm's value is set (the first arm must be the default); the
+    # others share one model
     models = {}
-    for a in (arms if args.key == "conv28_bn" else arms[:1]):
+    for a in (arms if args.key in PACKING_KEYS else arms[:1]):
         m = CViT(dtype=args.dtype)
         m.load_state_dict(sd)
         m.to(dev)
@@ -45,7 +49,7 @@ def main():
             next(iter(models.values())).set_option(args.key, a)
         m.reserve(8, dev)
         models[a] = m
-    model_of = (lambda a: models[a]) if args.key == "conv28_bn" else (lambda a: models[arms[0]])
+    model_of = (lambda a: models[a]) if args.key in PACKING_KEYS else (lambda a: models[arms[0]])
     for kv in args.pre:
         k, v = kv.split("=")
         model_of(arms[0]).set_option(k, int(v))
