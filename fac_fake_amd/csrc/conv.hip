@@ -84,6 +84,39 @@ __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, 
   }
 }
 
+// Epilogue part 1: folded-BN bias + ReLU (+ the 2x2 max of a window-major
+// row group) of a wave's RTW x CTW accumulator tiles -> 16-bit, into the LDS
+// staging tile (rows = window-major pixels, pitch OPS).  RELU is a template
+// argument (a runtime flag cost one v_cndmask per value), and the four rows
+// of a lane convert as two packed pairs (v_cvt_pk) written as the low and
+// high halves (ds_write_b16 / _d16_hi).
+template <class T, int RTW, int CTW, int OPS, bool POOL, bool RELU>
+__device__ __forceinline__ void stage_tile(const f32x4 (&acc)[RTW][CTW], uint16_t* ostg,
+                                           const float* __restrict__ bias_blk, int wm, int wn, int lane) {
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int nl = (wn * CTW + ct) * 16 + (lane & 15);
+    const float bv = bias_blk[nl];
+#pragma unroll
+    for (int rt = 0; rt < RTW; ++rt) {
+      const f32x4 v = acc[rt][ct];
+      if constexpr (POOL) {
+        const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])) + bv;
+        const int w = (wm * RTW + rt) * 4 + (lane >> 4);
+        ostg[w * OPS + nl] = T::from_f32(RELU ? relu(mx) : mx);
+      } else {
+        f32x4 y;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[j] = RELU ? relu(v[j] + bv) : v[j] + bv;
+        const u16x4 p = T::pack4(y);
+        const int m0 = (wm * RTW + rt) * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ostg[(m0 + j) * OPS + nl] = p[j];
+      }
+    }
+  }
+}
+
 // HB: halo buffers (2: the next chunk's halo streams in during this chunk;
 // 1: it is loaded between chunks, exposed, which halves the halo LDS so that
 // OCC = 3 workgroups share a CU and hide each other's exposed loads — the
@@ -369,26 +402,10 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // and conv6 203 -> 249 us: 16 8-byte stores of 32-byte segments per wave
   // against 8 fully coalesced 16-byte ones after the LDS transpose.)
   uint16_t* ostg = smem;
-#pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) {
-    const int nl = (wn * CTW + ct) * 16 + (lane & 15);
-    const float bv = bias[nb * BN + nl];
-#pragma unroll
-    for (int rt = 0; rt < RTW; ++rt) {
-      const f32x4 v = acc[rt][ct];
-      if constexpr (POOL) {
-        const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-        const int w = (wm * RTW + rt) * 4 + (lane >> 4);
-        ostg[w * OPS + nl] = T::from_f32(do_relu ? relu(mx + bv) : mx + bv);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int m = (wm * RTW + rt) * 16 + (lane >> 4) * 4 + j;
-          ostg[m * OPS + nl] = T::from_f32(do_relu ? relu(v[j] + bv) : v[j] + bv);
-        }
-      }
-    }
-  }
+  if (do_relu)
+    stage_tile<T, RTW, CTW, OPS, POOL, true>(acc, ostg, bias + nb * BN, wm, wn, lane);
+  else
+    stage_tile<T, RTW, CTW, OPS, POOL, false>(acc, ostg, bias + nb * BN, wm, wn, lane);
   __syncthreads();
   store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
 }
@@ -567,26 +584,10 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restric
   __syncthreads();
 
   uint16_t* ostg = smem;
-#pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) {
-    const int nl = (wn * CTW + ct) * 16 + (lane & 15);
-    const float bv = bias[nb * BN + nl];
-#pragma unroll
-    for (int rt = 0; rt < RTW; ++rt) {
-      const f32x4 v = acc[rt][ct];
-      if constexpr (POOL) {
-        const float mx = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-        const int w = (wm * RTW + rt) * 4 + (lane >> 4);
-        ostg[w * OPS + nl] = T::from_f32(do_relu ? relu(mx + bv) : mx + bv);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int m = (wm * RTW + rt) * 16 + (lane >> 4) * 4 + j;
-          ostg[m * OPS + nl] = T::from_f32(do_relu ? relu(v[j] + bv) : v[j] + bv);
-        }
-      }
-    }
-  }
+  if (do_relu)
+    stage_tile<T, RTW, CTW, OPS, POOL, true>(acc, ostg, bias + nb * BN, wm, wn, lane);
+  else
+    stage_tile<T, RTW, CTW, OPS, POOL, false>(acc, ostg, bias + nb * BN, wm, wn, lane);
   __syncthreads();
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const int oy0 = POOL ? y0 / 2 : y0, ox0 = POOL ? x0 / 2 : x0;
