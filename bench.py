@@ -500,6 +500,14 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     B = args.batch
+    if args.only and args.opt:
+        # process-wide knobs (conv_db, conv_wr, pool_impl) for the sub-measurement A/Bs
+        from fac_fake_amd.cvit import CViT
+        knobs = CViT(dtype=args.dtype)
+        knobs.reserve(1, dev)
+        for kv in args.opt:
+            k, v = kv.split("=")
+            knobs.set_option(k, int(v))
     if args.only == "resvitkan":
         r = resvitkan_measurement(dev, args.dtype, world, args.rvk_batch, steps=args.steps, warmup=args.warmup,
                                   chunk=args.stem_chunk if args.stem_chunk else None)

@@ -400,7 +400,10 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // global memory as 8 bytes, the 2x2 max by DPP across a window's 4 lanes.
   // Bit-identical outputs, but 2-23 % slower on every tile, conv4 165 -> 195
   // and conv6 203 -> 249 us: 16 8-byte stores of 32-byte segments per wave
-  // against 8 fully coalesced 16-byte ones after the LDS transpose.)
+  // against 8 fully coalesced 16-byte ones after the LDS transpose.  Also
+  // not kept: the same transposed MFMAs for the unpooled tiles with the LDS
+  // staging kept, one ds_write_b64 per tile instead of four ds_write_b16:
+  // bit-identical, per-layer sum 2350 -> 2359 us, CViT -1.2 % same box.)
   uint16_t* ostg = smem;
   if (do_relu)
     stage_tile<T, RTW, CTW, OPS, POOL, true>(acc, ostg, bias + nb * BN, wm, wn, lane);
