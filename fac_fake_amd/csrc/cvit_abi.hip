@@ -27,6 +27,8 @@ void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* ou
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, bool relu = true);
+hipError_t launch_conv45(int dtype, const uint16_t* in, const uint16_t* w4, const float* b4, const uint16_t* w5,
+                         const float* b5, uint16_t* out, int B, const uint16_t* zero16, hipStream_t st);
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
                         int B, int H, int W, hipStream_t st);
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
@@ -113,6 +115,7 @@ struct fac_ctx {
   int cap_B = 0;
   int stem_chunk = 0;
   int fuse_stem224 = 1;  // conv1..conv3+pool as one persistent kernel (stem224.hip)
+  int fuse45 = 0;        // 1: conv4 -> conv5 as one kernel (conv.hip conv45_fused; measured neutral, off)
   // GEMM tile variant per call site (transformer.hip launch_gemm; -1 = default)
   // and the split-K factor of the two N=1024 projections (to_out, FF2)
   int gemm_var[6] = {-1, -1, -1, -1, -1, -1};  // patch, qkv, out, ff1, ff2, head
@@ -563,6 +566,21 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
       }
     }
     for (int l = l0; l <= kLastChunked && !copied; ++l) {
+      if (l == 2 && c->fuse45 && stop_after != 3) {
+        // conv4 -> conv5 in one launch (conv4's output stays in LDS)
+        HIP_TRY(c, launch_conv45(dt, cur, c->conv[2].w, c->conv[2].b, c->conv[3].w, c->conv[3].b, nxt, nb, c->zero16,
+                                 st));
+        MARK(3);
+        MARK(4);
+        if (stop_after == 4) {
+          HIP_TRY(c, hipMemcpyAsync(feat_out + (size_t)b0 * conv_out_elems(c->conv[3]), nxt,
+                                    (size_t)nb * conv_out_elems(c->conv[3]) * 2, hipMemcpyDeviceToDevice, st));
+          copied = true;
+        }
+        std::swap(cur, nxt);
+        ++l;
+        continue;
+      }
       const ConvLayer& L = c->conv[l];
       uint16_t* dst = (l == kLastChunked) ? c->deep0 + (size_t)b0 * conv_out_elems(L) : nxt;
       HIP_TRY(c, run_conv(c, L, cur, dst, nb, st));
@@ -725,6 +743,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "stem_events") {
     c->stem_ev = value != 0;
     c->stem_ev_used = 0;
+    return FAC_OK;
+  }
+  if (k == "fuse45") {  // 1: conv4 -> conv5 fused (conv45_fused); 0 (default): two launches
+    c->fuse45 = value != 0;
     return FAC_OK;
   }
   if (k == "conv_db") {  // 1 (default): conv3x3_db for the 28^2 tiles; 0: the LDS weight ring (A/B); process-wide

@@ -194,7 +194,10 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48), "conv_db" (1 = the
  * 28x28 3x3 convs fetch their weight fragments straight into registers,
  * conv3x3_db, the default; 0 = through the LDS weight ring; bit-identical
- * outputs; process-wide, for A/B measurements). */
+ * outputs; process-wide, for A/B measurements), "fuse45" (1 = conv4 -> conv5
+ * as one kernel, conv4 recomputed on each box's halo in LDS; 0 = two
+ * launches, the default: the fused kernel measured neutral, DESIGN.md §3.4;
+ * bit-identical outputs). */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);

@@ -189,6 +189,37 @@ def test_fused_stem224_vs_unfused_and_oracle(models, sd, dt, torch_threads):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_conv45_fused_equals_unfused(models, dt):
+    """conv4 -> conv5 as one kernel (option fuse45, off by default: measured
+    neutral; conv45_fused: conv4 recomputed on each
+    box's 18x18 halo in LDS, rounded to 16 bits exactly where the unfused
+    path stores it, then conv5 with the same k order): conv5's output, the
+    stem's output and the logits are bit-identical to the two-launch path,
+    on crops whose boxes cover every image border (n = 7: 343 boxes)."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models[dt]
+    n = 7
+    x = torch.from_numpy(make_crops(n, seed=45)).to(DEV)
+    tdt = torch.float16 if dt == "fp16" else torch.bfloat16
+    pidx = (torch.arange(n, device=DEV) % 32).to(torch.int32)
+    outs = {}
+    for fuse in (1, 0):
+        _lib.check(lib.fac_set_option(m._ctx, b"fuse45", fuse), m._ctx, "opt")
+        c5 = torch.empty(n, 112, 112, 64, dtype=tdt, device=DEV)
+        _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), n, 4, c5.data_ptr(), None), m._ctx, "dbg")
+        st = torch.empty(n, 7, 7, 512, dtype=tdt, device=DEV)
+        _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), n, 16, st.data_ptr(), None), m._ctx, "dbg")
+        with torch.no_grad():
+            lg = m.forward_u8(x, pos_index=pidx)
+        torch.cuda.synchronize()
+        outs[fuse] = (c5.view(torch.int16).cpu(), st.view(torch.int16).cpu(), lg.cpu())
+    _lib.check(lib.fac_set_option(m._ctx, b"fuse45", 0), m._ctx, "opt")
+    for a, b in zip(outs[1], outs[0]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
 def test_tail_isolated(models, sd, dt, torch_threads):
     """Patch embedding + 6 transformer layers + head from the oracle's stem
     output: within the 16-bit rounding envelope of the fp32 tail."""
