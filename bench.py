@@ -250,6 +250,14 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         recs.append((flops, byts))
         return out
 
+    orig_s2dc = ops.conv_s2d4_clip
+
+    def s2dc_hook(layer, clip, **kw):   # S3D's first conv with the s2d packing folded in: fp32 clip in
+        out = orig_s2dc(layer, clip, **kw)
+        M = out.numel() // layer.cout
+        recs.append((2.0 * M * layer.cout * layer.g.kh * layer.g.kw * layer.cin, 4.0 * clip.numel() + 2.0 * out.numel()))
+        return out
+
     orig_dual = ops.conv_dual
 
     def dual_hook(layer, h, ds, x, **kw):   # conv3 + fused downsample: one op, its own minimum bytes
@@ -285,6 +293,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         return out
 
     ops.ConvLayer.__call__ = conv_hook
+    ops.conv_s2d4_clip = s2dc_hook
     ops.conv_dual = resvitkan.conv_dual = dual_hook
     ops.bottleneck_pw2 = resvitkan.bottleneck_pw2 = pw2_hook
     ops.pool = resvitkan.pool = s3d.pool = pool_hook
@@ -294,6 +303,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         torch.cuda.synchronize()
     finally:
         ops.ConvLayer.__call__ = orig_call
+        ops.conv_s2d4_clip = orig_s2dc
         ops.conv_dual = resvitkan.conv_dual = orig_dual
         ops.bottleneck_pw2 = resvitkan.bottleneck_pw2 = orig_pw2
         ops.pool = resvitkan.pool = s3d.pool = orig_pool

@@ -59,6 +59,8 @@ SIGNATURES = {
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     # include/fac_ops.h
     "fac_conv_nd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "fac_conv_s2d4_clip": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p]),
     "fac_conv_nd_dual": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_bottleneck_pw2": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "fac_conv_weight_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -131,6 +133,12 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def exports(name: str) -> bool:
+    """Whether the loaded library has entry point `name` (only an older build
+    selected with FAC_CVIT_LIB for an A/B run can lack one)."""
+    return isinstance(getattr(load(), name), ctypes._CFuncPtr)
 
 
 class FacError(RuntimeError):

@@ -793,10 +793,20 @@ __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, fl
 // k-step s covers taps 2s, 2s+1 (ty = s/2, tx = 2(s%2) + g/2) x 16 channels:
 // lane group g reads channel piece g%2 of tap 2s + g/2, i.e. k = 32s + 8g + e,
 // the natural fac_conv_nd weight order.
-template <class T>
-__global__ __launch_bounds__(256, 2) void conv_s2d4(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+// F32IN (round 4): `in` is S3D's raw fp32 clip batch
+// [clip][3][frames][H][W] and the cells are made while staging each box's
+// halo -- fac_pack_input_s2d's 16-bit cell image (1.12 GB per 384-clip
+// forward written and read back) never exists.  A lane's pieces are fetched
+// as three 8-byte float pairs (one per colour plane; a piece is one pixel row
+// of a cell: 2 pixels x 3 channels + 2 zeros) into registers one box ahead,
+// and converted + written to the other halo buffer after this box's MFMAs
+// and stores; plain loads only, so the compiler's vmcnt waits are exact.
+template <class T, bool F32IN = false>
+__global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_, const uint16_t* __restrict__ w,
                                                     const float* __restrict__ bias, uint16_t* __restrict__ out,
-                                                    int nbox, int Hc, int Wc, int Ho, int Wo, int kp, int relu_on) {
+                                                    int nbox, int Hc, int Wc, int Ho, int Wo, int kp, int relu_on,
+                                                    int frames = 1, int H = 0, int W = 0, int pb = 0) {
+  const uint16_t* __restrict__ in = (const uint16_t*)in_;
   constexpr int TH = 8, TW = 28, HH = TH + 3, HWD = TW + 3, RPX = 32;  // halo rows, cols, row pitch (cells)
   constexpr int HSL = 2 * HH * RPX;                                       // 16-byte halo slots
   constexpr int HPW = (HSL + 255) / 256;                                  // glds per wave
@@ -849,25 +859,81 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const uint16_t* __restrict__
       glds16(src, halo + (i * 4 + wave) * 64 * 8);
     }
   };
+  // F32IN: this lane's cell pieces p = tid + 256 j of the dense 2 x 11 x 31
+  // halo (piece 0 / 1 = the cell's top / bottom pixel row), as raw float pairs
+  constexpr int NPC = 2 * HH * HWD, PPL = (NPC + 255) / 256;
+  float2 raw[F32IN ? PPL : 1][3];
+  auto load_raw = [&](int bx) {
+    const int img = bx / bpi, rr = bx - img * bpi;
+    const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
+    const int clip = img / frames, f = img - clip * frames;
+    const float* src = (const float*)in_ + (size_t)clip * 3 * frames * H * W + (size_t)f * H * W;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = tid + 256 * j;
+      const int pc = p / (HH * HWD), rem = p - pc * (HH * HWD), hy = rem / HWD, hx = rem - (rem / HWD) * HWD;
+      const int Y = y0 + hy, X = x0 + hx, y = 2 * (Y - pb) + pc, x = 2 * (X - pb);
+      const bool ok = p < NPC && Y >= pb && X >= pb && y < H && x < W;
+      const size_t off = ok ? (size_t)y * W + x : 0;  // branch-free: masked pieces read pixel 0 and are zeroed
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float2 v = *(const float2*)(src + (size_t)c * frames * H * W + off);
+        raw[j][c] = ok ? v : make_float2(0.f, 0.f);
+      }
+    }
+  };
+  auto store_cells = [&](uint16_t* halo) {
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = tid + 256 * j;
+      if (p < NPC) {
+        const int pc = p / (HH * HWD), rem = p - pc * (HH * HWD), hy = rem / HWD, hx = rem - (rem / HWD) * HWD;
+        u16x8 v;
+        v[0] = T::from_f32(raw[j][0].x);
+        v[1] = T::from_f32(raw[j][1].x);
+        v[2] = T::from_f32(raw[j][2].x);
+        v[3] = 0;
+        v[4] = T::from_f32(raw[j][0].y);
+        v[5] = T::from_f32(raw[j][1].y);
+        v[6] = T::from_f32(raw[j][2].y);
+        v[7] = 0;
+        *(u16x8*)(halo + ((pc * HH + hy) * RPX + hx) * 8) = v;
+      }
+    }
+  };
   __syncthreads();  // weights in
-  if (blockIdx.x < nbox) issue(blockIdx.x, smem + WEL);
+  if constexpr (F32IN) {
+    if (blockIdx.x < nbox) {
+      load_raw(blockIdx.x);
+      store_cells(smem + WEL);
+      if (blockIdx.x + (int)gridDim.x < nbox) load_raw(blockIdx.x + gridDim.x);
+    }
+  } else {
+    if (blockIdx.x < nbox) issue(blockIdx.x, smem + WEL);
+  }
   int it = 0;
   for (int bx = blockIdx.x; bx < nbox; bx += gridDim.x, ++it) {
     const int img = bx / bpi, rr = bx - img * bpi;
     const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
     uint16_t* const halo = smem + WEL + (it & 1) * HEL;
     const bool more = bx + (int)gridDim.x < nbox;
-    // every wave is done with the other buffer (the previous box): refill it
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (more) issue(bx + gridDim.x, smem + WEL + ((it + 1) & 1) * HEL);
-    // this box's halo landed; younger: the next box's pieces (if any) and,
-    // after the first box, the previous box's 7 stores
-    if (it == 0) {
-      if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (F32IN) {
+      // this box's cells are written (the previous iteration / the prologue)
+      // and every wave is done with the other buffer
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     } else {
-      if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW + 7) : "memory");
-      else asm volatile("s_waitcnt vmcnt(7)\n\ts_barrier" ::: "memory");
+      // every wave is done with the other buffer (the previous box): refill it
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (more) issue(bx + gridDim.x, smem + WEL + ((it + 1) & 1) * HEL);
+      // this box's halo landed; younger: the next box's pieces (if any) and,
+      // after the first box, the previous box's 7 stores
+      if (it == 0) {
+        if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        if (more) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(HPW + 7) : "memory");
+        else asm volatile("s_waitcnt vmcnt(7)\n\ts_barrier" ::: "memory");
+      }
     }
     f32x4 acc[7][2];
 #pragma unroll
@@ -898,6 +964,15 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const uint16_t* __restrict__
         q[ct] = T::pack4(v);
       }
       *(u16x8*)o = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    if constexpr (F32IN) {
+      // the next box's cells into the other buffer (its float pairs were
+      // fetched one box ago; this box's stores stay in flight), then the
+      // box after next's float pairs
+      if (more) {
+        store_cells(smem + WEL + ((it + 1) & 1) * HEL);
+        if (bx + 2 * (int)gridDim.x < nbox) load_raw(bx + 2 * gridDim.x);
+      }
     }
   }
 }
@@ -2436,6 +2511,41 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
 
 int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   return conv_nd_impl(d, nullptr, 0, INT_MAX, nullptr, 0, INT_MAX, stream);
+}
+
+int fac_conv_s2d4_clip(const fac_conv_desc* d, const float* clip, int h, int w, int pad_before, void* stream) {
+  using namespace fac;
+  if (!d || !clip || !d->weight || !d->out || (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16))
+    return FAC_ERR_ARG;
+  if ((d->flags & ~FAC_CONV_RELU) != 0 || h <= 0 || w <= 0 || h % 2 || w % 2 || pad_before < 0 || d->n <= 0 ||
+      d->d <= 0)
+    return FAC_ERR_ARG;
+  int cout_pad, k_pad;
+  fac_conv_weight_layout(d->cout, d->cin, d->kd, d->kh, d->kw, &cout_pad, &k_pad);
+  // the conv fac_conv_nd would run on fac_pack_input_s2d(clip)'s cells: 4x4/1
+  // over 16-channel cells, cout 64, no padding, dense output, 8x28 boxes
+  const bool shape = d->kd == 1 && d->kh == 4 && d->kw == 4 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+                     d->pd == 0 && d->ph == 0 && d->pw == 0 && d->cin == 16 && d->cout == 64 && d->k_pad == k_pad &&
+                     k_pad == 256 && d->od == d->d && d->oh == d->h - 3 && d->ow == d->w - 3 && d->oh % 8 == 0 &&
+                     d->ow % 28 == 0 && d->ldo == 64 && d->c_off == 0 && d->h >= h / 2 + pad_before &&
+                     d->w >= w / 2 + pad_before;
+  if (!shape) return FAC_ERR_SHAPE;
+  if ((long long)d->n * d->d * 3 * h * w >= (1LL << 40)) return FAC_ERR_SHAPE;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const int nimg = d->n * d->od, nbox = nimg * (d->oh / 8) * (d->ow / 28);
+  const int grid = std::min(nbox, 2 * ncu);
+  const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == FAC_DTYPE_BF16)
+    conv_s2d4<BF16, true><<<grid, 256, 0, st>>>(clip, (const uint16_t*)d->weight, d->bias, (uint16_t*)d->out, nbox,
+                                                d->h, d->w, d->oh, d->ow, k_pad, relu_on, d->d, h, w, pad_before);
+  else
+    conv_s2d4<F16, true><<<grid, 256, 0, st>>>(clip, (const uint16_t*)d->weight, d->bias, (uint16_t*)d->out, nbox,
+                                               d->h, d->w, d->oh, d->ow, k_pad, relu_on, d->d, h, w, pad_before);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 
 int fac_conv_nd_split(const fac_conv_desc* d, void* out1, int ldo1, int split1, void* out2, int ldo2, int split2,

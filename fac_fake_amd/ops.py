@@ -401,6 +401,36 @@ def pack_input_s2d(src: torch.Tensor, *, dtype: str, u8: bool, div: float = 1.0,
     return out
 
 
+def conv_s2d4_clip(layer: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2, pad_after: int = 1,
+                   relu: bool = True) -> torch.Tensor:
+    """``layer(pack_input_s2d(clip, u8=False, pad_before, pad_after))`` in one
+    launch (fac_conv_s2d4_clip): S3D's base.0 spatial (1,7,7)/(1,2,2) conv
+    (model.py:18) with the space-to-depth packing folded into the conv's halo
+    staging, so the 16-bit cell image never goes through HBM.  ``clip`` is the
+    fp32 batch [N, 3, T, h, w]; ``layer`` the s2d-weight 4x4 conv.
+    Bit-identical to the two launches."""
+    if clip.dtype != torch.float32 or clip.dim() != 5 or clip.shape[1] != 3 or not clip.is_contiguous():
+        raise ValueError(f"expected a contiguous fp32 clip [N,3,T,H,W], got {clip.dtype} {tuple(clip.shape)}")
+    n, _, t, h, w = clip.shape
+    hc, wc = h // 2 + pad_before + pad_after, w // 2 + pad_before + pad_after
+    od, oh, ow = layer.out_dims(t, hc, wc)
+    out = torch.empty(n, od, oh, ow, layer.cout, device=clip.device, dtype=TORCH16[layer.dtype])
+    g = layer.g
+    dsc = ConvDesc()
+    dsc.dtype = _lib.DTYPES[layer.dtype]
+    dsc.n, dsc.d, dsc.h, dsc.w, dsc.cin = n, t, hc, wc, layer.cin_p
+    dsc.weight, dsc.bias = layer.w.data_ptr(), layer.b.data_ptr()
+    dsc.cout, dsc.k_pad = layer.cout, layer.k_pad
+    dsc.kd, dsc.kh, dsc.kw, dsc.sd, dsc.sh, dsc.sw = g.kd, g.kh, g.kw, g.sd, g.sh, g.sw
+    dsc.pd, dsc.ph, dsc.pw = g.pd, g.ph, g.pw
+    dsc.od, dsc.oh, dsc.ow = od, oh, ow
+    dsc.out, dsc.ldo, dsc.c_off = out.data_ptr(), layer.cout, 0
+    dsc.flags = RELU if relu else 0
+    _lib.check(_lib.load().fac_conv_s2d4_clip(ctypes.byref(dsc), clip.data_ptr(), h, w, pad_before, _stream(clip)),
+               None, "fac_conv_s2d4_clip")
+    return out
+
+
 def s2d_weight(w: torch.Tensor) -> torch.Tensor:
     """[co, 3, 7, 7] stride-2 pad-3 kernel -> [co, 16, 4, 4] stride-1 kernel over
     fac_pack_input_s2d cells: w'[o][(dy*2+dx)*4 + c][ty][tx] = w[o][c][2ty+dy-1][2tx+dx-1].

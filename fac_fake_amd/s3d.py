@@ -28,6 +28,7 @@ from torch import nn
 
 from . import _lib
 from .cvit import _Node
+from . import ops
 from .ops import TORCH16, ConvLayer, conv_split, fold_bn, max_pool_sep, pack_input, pack_input_s2d, pool, s2d_weight, sigmoid
 from .weights import s3d_base, s3d_param_specs
 
@@ -131,7 +132,7 @@ class S3D(nn.Module):
         for i, L in enumerate(s3d_base(self._srm)):
             p = f"base.{i}"
             if L[0] == "sep" and i == 0 and not self._srm:
-                self._layers.append(("sep", sep_s2d(p)))
+                self._layers.append(("sep_s2d", sep_s2d(p)))
             elif L[0] == "sep":
                 self._layers.append(("sep", sep(p, L[3], L[4], L[5], cin_pad=32 if i == 0 else None)))
             elif L[0] == "basic":
@@ -228,7 +229,8 @@ class S3D(nn.Module):
         return out
 
     def features16(self, x16: torch.Tensor, taps: list | None = None) -> torch.Tensor:
-        """`base` (model.py:17-33) on the packed clip -> [B, T', H', W', 1024] 16-bit.
+        """`base` (model.py:17-33) on the packed clip (`_pack`: without SRM the
+        raw fp32 clip, or its ops.pack_input_s2d cells) -> [B, T', H', W', 1024] 16-bit.
         With `taps`, the output of every base[i] ([B, T, H, W, C] channels-last,
         16-bit) is appended to it, in order."""
         y = x16
@@ -237,7 +239,12 @@ class S3D(nn.Module):
             s = torch.zeros(n, d, h, w, 32, dtype=y.dtype, device=y.device)   # 30 filters + 2 zero channels
             y = self._srm_conv(y, relu=False, out=s)
         for kind, L in self._layers:
-            if kind == "sep":
+            if kind == "sep_s2d":
+                # the raw fp32 clip (`_pack`): the space-to-depth packing runs
+                # inside the conv's halo staging (ops.conv_s2d4_clip); packed
+                # cells (ops.pack_input_s2d) still take the plain conv
+                y = L[1](ops.conv_s2d4_clip(L[0], y) if y.dtype == torch.float32 else L[0](y))
+            elif kind == "sep":
                 y = L[1](L[0](y))
             elif kind == "basic":
                 y = L(y)
@@ -258,6 +265,9 @@ class S3D(nn.Module):
         _, _, T, H, W = x.shape
         if self._srm:
             return pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
+        # base.0's space-to-depth cells are made inside its conv (ops.conv_s2d4_clip)
+        if _lib.exports("fac_conv_s2d4_clip"):
+            return x.float().contiguous()
         return pack_input_s2d(x.float(), dtype=self.dtype_name, u8=False, pad_before=2, pad_after=1)
 
     def base_outputs(self, x: torch.Tensor) -> list:

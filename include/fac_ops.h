@@ -159,6 +159,15 @@ int fac_pack_input(int dtype, const void* src, int src_kind, int n, int s, float
 int fac_pack_input_s2d(int dtype, const void* src, int src_kind, int n, int frames, int h, int w, int pad_before,
                        int pad_after, float div, const float* mean3, const float* std3, void* out, void* stream);
 
+/* fac_conv_nd over fac_pack_input_s2d(src_kind 1, div 1, no mean / std)'s
+ * cells of the fp32 clip batch `clip` [n][3][frames][h][w], with the packing
+ * folded into the conv's halo staging (S3D's base.0 spatial conv,
+ * model.py:18): `desc` describes that conv exactly as fac_conv_nd would get
+ * it (cells [n][frames][h/2+pad_before+pad_after]^2[16], the 4x4/1 cout-64
+ * s2d kernel, flags 0 or FAC_CONV_RELU); desc->in is not read.  The output
+ * is bit-identical to fac_pack_input_s2d + fac_conv_nd. */
+int fac_conv_s2d4_clip(const fac_conv_desc* desc, const float* clip, int h, int w, int pad_before, void* stream);
+
 /* KANLinear forward (CViT-main/ResVitKan/kan.py:189-206), fp32:
  *   y = silu(x) · base_weightᵀ + b_splines(x) · (spline_weight ⊙ spline_scaler)ᵀ
  * with order-3 B-spline bases over the per-feature knot vector `grid`

@@ -133,6 +133,28 @@ def test_bottleneck_pw2_matches_two_launches(cin, cmid, n1, hw, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("n,t,relu", [(2, 3, True), (4, 10, False), (20, 8, True)])
+def test_conv_s2d4_clip_equals_pack_then_conv(n, t, relu, dt):
+    """fac_conv_s2d4_clip (S3D's base.0 spatial conv with the space-to-depth
+    packing folded into the halo staging, fp32 clip in) against
+    fac_pack_input_s2d + fac_conv_nd: bit-identical, for raw 0..255 clips,
+    one box per workgroup (n*t*14 = 84 boxes), a few (560) and several (2240)
+    boxes per persistent workgroup (the register prefetch of the next box's
+    pixels and the double-buffered cells), with and without ReLU."""
+    from fac_fake_amd.ops import ConvLayer, conv_s2d4_clip, pack_input_s2d, s2d_weight
+    g = torch.Generator().manual_seed(n + t)
+    clip = (torch.rand(n, 3, t, 112, 112, generator=g) * 255).to(DEV)
+    wt = torch.randn(64, 3, 1, 7, 7, generator=g) / 12
+    b = torch.randn(64, generator=g) * 0.5
+    layer = ConvLayer(s2d_weight(wt), b, 1, 0, dtype=dt, device=DEV)
+    fused = conv_s2d4_clip(layer, clip, relu=relu)
+    ref = layer(pack_input_s2d(clip, dtype=dt, u8=False, pad_before=2, pad_after=1), relu=relu)
+    torch.cuda.synchronize()
+    assert tuple(fused.shape) == (n, t, 56, 56, 64)
+    assert torch.equal(fused.view(torch.int16).cpu(), ref.view(torch.int16).cpu())
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("n,d,h,w", [(2, 1, 19, 59), (1, 2, 35, 31), (3, 1, 115, 115), (300, 1, 19, 59)])
 def test_conv_s2d4_maxpool_fused(n, d, h, w, dt):
     """conv_s2d4_mp (FAC_CONV_MAXPOOL3S2): the 4x4/1 space-to-depth conv +
