@@ -72,6 +72,9 @@ __device__ __forceinline__ void trk_norm(Trk& t, int C8, int KH, int KW) {
 
 // 16 zero bytes: the glds source of padding / out-of-range K pieces
 __device__ const uint16_t g_zero16[64] = {0};
+// write-only target of stores that must issue but whose values nobody reads
+// (convnd_pt's padding channels, bneck_pw2's rows past M): 16 bytes per lane
+__device__ uint16_t g_sink[64 * 8];
 
 // Async global -> LDS copy of 16 bytes per lane (global_load_lds_dwordx4):
 // the wave's 64 pieces land contiguously at the wave-uniform LDS address.
@@ -1164,7 +1167,6 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4_mp(const uint16_t* __restric
 // Rows past M (a partial last tile) load row M-1 and store into g_sink, so
 // every load and store is unconditional: the compiler's wait for the next
 // tile's registers then counts this tile's stores instead of draining them.
-__device__ uint16_t g_sink[64 * 8];
 
 template <class T, int N1>
 __global__ __launch_bounds__(512, 1) void bneck_pw2(const uint16_t* __restrict__ a, const uint16_t* __restrict__ w3,
@@ -1938,7 +1940,9 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
   const int G = gridDim.x;
   int b = blockIdx.x;
   if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);  // consecutive b on one XCD
-  const int ny = p.Cout / BN, nrt = (p.M + BM - 1) / BM;
+  // column blocks: the last one partial when BN does not divide Cout (its
+  // weight rows and biases past Cout are padding, its stores go to g_sink)
+  const int ny = (p.Cout + BN - 1) / BN, nrt = (p.M + BM - 1) / BM;
   const int cb = b % ny, rstep = G / ny;
   const int n0 = cb * BN;
   int rt_first = b / ny;
@@ -1963,7 +1967,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
   for (int c = tid; c < NBIAS; c += 512) {
     const float* bsrc = c < BN ? p.bias : q.bias;
     const int cc = c < BN ? c : c - BN;
-    sbias[c] = bsrc ? bsrc[n0 + cc] : 0.f;
+    sbias[c] = bsrc && n0 + cc < p.Cout ? bsrc[n0 + cc] : 0.f;
   }
   __syncthreads();
   // this lane's 4 channels of channel tile ct (second = q's biases)
@@ -2166,6 +2170,7 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
         const int m = c_rt * BM + wm * WTM + rt * 16 + r16;
         if (m < p.M) {
           uint16_t* o = (uint16_t*)p.out + (size_t)m * p.ldo + p.c_off + n0 + wn * 64 + 8 * g;
+          const int ch = n0 + wn * 64 + 8 * g;
 #pragma unroll
           for (int pp = 0; pp < CT / 2; ++pp) {
             u16x4 q2[2];
@@ -2191,7 +2196,11 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
               }
               q2[h] = T::pack4(v);
             }
-            *(u16x8*)(o + 32 * pp) = __builtin_shufflevector(q2[0], q2[1], 0, 1, 2, 3, 4, 5, 6, 7);
+            // channels past Cout (a partial column block): the store still
+            // issues, into g_sink, so every tile counts NST stores in the
+            // vmcnt waits above
+            uint16_t* dst = ch + 32 * pp < p.Cout ? o + 32 * pp : g_sink + 8 * lane;
+            *(u16x8*)dst = __builtin_shufflevector(q2[0], q2[1], 0, 1, 2, 3, 4, 5, 6, 7);
           }
         }
 #pragma unroll
@@ -2217,22 +2226,33 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
   return dim3(gx, ny);
 }
 
+// process-wide (fac_set_option "nd_pt_wide"): convnd_pt also for cout not a
+// multiple of 128 (a partial last column block) from this many 256-row tiles
+// on; 0 keeps those on convnd_igemm (A/B)
+static int g_nd_pt_wide = 1024;
+void set_nd_pt_wide(int v) { g_nd_pt_wide = v; }
+
 template <class T>
 static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
   const bool res = p.flags & FAC_CONV_RESID;
-  if (p.Cout % 128 || p.ksteps < 2 || !p.vec_out || p.split1 < p.Cout ||
+  if (p.ksteps < 2 || !p.vec_out || p.split1 < p.Cout || p.Cout % 8 ||
       (p.flags & FAC_CONV_OUT_F32) || (!res && (p.flags & FAC_CONV_RELU2)) || (res && !p.vec_res))
     return false;
+  const int nrt = (p.M + 255) / 256;
+  if (p.Cout % 128) {
+    // partial column block: no residual tile, and enough row tiles that
+    // every persistent workgroup walks several (small late-block grids keep
+    // convnd_igemm's 64 x 64 tiles)
+    if (!g_nd_pt_wide || res || nrt < g_nd_pt_wide) return false;
+  }
   static const int ncu = [] {
     int dev = 0, n = 256;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       n = 256;
     return n;
   }();
-  const int nrt = (p.M + 255) / 256;
   const int bn = res ? 128 : (p.Cout % 256 == 0 ? 256 : 128);
-  if (p.Cout % bn) return false;
-  const int ny = p.Cout / bn;
+  const int ny = (p.Cout + bn - 1) / bn;
   int G = ncu / ny * ny;
   if ((long long)nrt * ny < G) G = nrt * ny;
   if (G <= 0) return false;

@@ -159,7 +159,13 @@ class S3D(nn.Module):
                 # (3,1,1) halves take the uniform-tap gather too
                 m1 = (b1b + 63) // 64 * 64 if self.padt else b1b
                 m2 = (b2b + 63) // 64 * 64 if self.padt else b2b
-                b1, b2 = sep(f"{p}.branch1.1", 3, 1, 1), sep(f"{p}.branch2.1", 3, 1, 1)
+                # at 14x14 and above, branch2's SepConv middle channels 96 ->
+                # 128 (zero rows of the (1,3,3) half): that half then has a
+                # conv.hip tile and the (3,1,1) half reads a uniform-tap K
+                # (convnd_pt with a partial column block). Mixed_3c, 384 clips:
+                # 327 -> 160 us (tools/s3d_small_ab.py); 32 -> 64 is slower
+                m2w = (b2b + 127) // 128 * 128 if b2b > 64 and b2b % 64 else None
+                b1, b2 = sep(f"{p}.branch1.1", 3, 1, 1), sep(f"{p}.branch2.1", 3, 1, 1, mid_pad=m2w)
 
                 def padded(p=p, heads=heads, merged=merged, b1=b1, b2=b2, b1a=b1a, b1b=b1b, b2a=b2a, b2b=b2b,
                            p1=p1, p2=p2, m1=m1, m2=m2):

@@ -96,6 +96,60 @@ def test_conv_nd_vs_torch_fp32(case, dt):
     assert (u > 0).float().mean() <= 0.05
 
 
+def _nd_pt_wide(value: int, dt: str):
+    """fac_set_option("nd_pt_wide") is process-wide; any context sets it."""
+    import ctypes
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    _lib.check(lib.fac_create(0, _lib.DTYPES[dt], ctypes.byref(h)), None, "fac_create")
+    try:
+        _lib.check(lib.fac_set_option(h, b"nd_pt_wide", value), h, "fac_set_option")
+    finally:
+        lib.fac_destroy(h)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("n,d,h,w,cin,cout,k,pd,c_off", [
+    (2, 8, 14, 14, 128, 96, (3, 1, 1), (1, 0, 0), 0),      # S3D Mixed_3c branch2 (3,1,1) half, mid padded
+    (3, 1, 23, 29, 192, 32, (1, 1, 1), 0, 8),              # cout 32 into a channel slot of a wider tensor
+    (2, 3, 7, 7, 128, 200, (1, 3, 3), (0, 1, 1), 0),       # two column blocks, the second 72 wide
+    (1, 5, 9, 13, 64, 136, (3, 3, 3), 1, 16),              # 3-D taps, partial row tile, c_off
+])
+def test_conv_nd_pt_partial_column_block(n, d, h, w, cin, cout, k, pd, c_off, dt):
+    """convnd_pt with cout % 128 != 0 (a partial last column block whose
+    padding channels store into a sink, so the hand-counted vmcnt waits still
+    see every store): forced onto these small shapes with nd_pt_wide = 1 (any
+    row-tile count), against torch's fp32 conv (one 16-bit ulp) and against
+    the convnd_igemm route (nd_pt_wide = 0), and the channels around the
+    written slot left untouched."""
+    from fac_fake_amd.ops import ConvLayer
+    g = torch.Generator().manual_seed(cin + cout)
+    x = torch.randn(n, cin, d, h, w, generator=g).to(T16[dt]).float()
+    wt = (torch.randn(cout, cin, *k, generator=g) / np.sqrt(cin * np.prod(k))).float()
+    b = torch.randn(cout, generator=g) * 0.1
+    layer = ConvLayer(wt, b, 1, pd, dtype=dt, device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    od, oh, ow = layer.out_dims(d, h, w)
+    outs = {}
+    try:
+        for v in (1, 0):
+            _nd_pt_wide(v, dt)
+            o = torch.full((n, od, oh, ow, c_off + cout + 8), 7.0, device=DEV, dtype=T16[dt])
+            layer(xg, relu=True, out=o, c_off=c_off)
+            torch.cuda.synchronize()
+            outs[v] = o.cpu()
+    finally:
+        _nd_pt_wide(1024, dt)
+    y = outs[1]
+    assert torch.all(y[..., :c_off] == 7.0) and torch.all(y[..., c_off + cout:] == 7.0)
+    ref = F.relu(F.conv3d(x, wt.to(T16[dt]).float(), b, padding=pd)).permute(0, 2, 3, 4, 1)
+    u = _ulps(y[..., c_off:c_off + cout], ref.to(T16[dt]), dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05
+    u2 = _ulps(y, outs[0], dt)
+    assert u2.max() <= 1.0 and (u2 > 0).float().mean() <= 0.05
+
+
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("cin,cmid,n1,hw", [(64, 256, 64, (56, 56)), (64, 256, 128, (23, 29)),
                                             (128, 512, 128, (28, 28)), (128, 512, 128, (13, 11))])
