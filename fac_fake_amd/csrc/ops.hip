@@ -2198,8 +2198,13 @@ __global__ __launch_bounds__(512, 1) void convnd_pt(ConvP p, ConvP q) {
             }
             // channels past Cout (a partial column block): the store still
             // issues, into g_sink, so every tile counts NST stores in the
-            // vmcnt waits above
-            uint16_t* dst = ch + 32 * pp < p.Cout ? o + 32 * pp : g_sink + 8 * lane;
+            // vmcnt waits above.  Column segments (fac_conv_nd_split, 8-aligned):
+            // [split1, split2) -> out1 (ldo1), [split2, cout) -> out2 (ldo2)
+            const int cg = ch + 32 * pp;
+            uint16_t* dst = cg >= p.Cout    ? g_sink + 8 * lane
+                            : cg >= p.split2 ? (uint16_t*)p.out2 + (size_t)m * p.ldo2 + (cg - p.split2)
+                            : cg >= p.split1 ? (uint16_t*)p.out1 + (size_t)m * p.ldo1 + (cg - p.split1)
+                                             : o + 32 * pp;
             *(u16x8*)dst = __builtin_shufflevector(q2[0], q2[1], 0, 1, 2, 3, 4, 5, 6, 7);
           }
         }
@@ -2235,14 +2240,15 @@ void set_nd_pt_wide(int v) { g_nd_pt_wide = v; }
 template <class T>
 static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
   const bool res = p.flags & FAC_CONV_RESID;
-  if (p.ksteps < 2 || !p.vec_out || p.split1 < p.Cout || p.Cout % 8 ||
+  const bool split = p.split1 < p.Cout;
+  if (p.ksteps < 2 || !p.vec_out || p.Cout % 8 || (split && res) ||
       (p.flags & FAC_CONV_OUT_F32) || (!res && (p.flags & FAC_CONV_RELU2)) || (res && !p.vec_res))
     return false;
   const int nrt = (p.M + 255) / 256;
-  if (p.Cout % 128) {
-    // partial column block: no residual tile, and enough row tiles that
-    // every persistent workgroup walks several (small late-block grids keep
-    // convnd_igemm's 64 x 64 tiles)
+  if (p.Cout % 128 || split) {
+    // a partial column block or column segments (fac_conv_nd_split): no
+    // residual tile, and enough row tiles that every persistent workgroup
+    // walks several (small late-block grids keep convnd_igemm's tiles)
     if (!g_nd_pt_wide || res || nrt < g_nd_pt_wide) return false;
   }
   static const int ncu = [] {

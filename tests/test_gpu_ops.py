@@ -596,12 +596,24 @@ def test_s3d_graph_replay_matches_eager(s3d_models):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
-def test_conv_split_equals_separate_convs(dt):
+@pytest.mark.parametrize("pt_wide,shape", [(1024, (2, 4, 7, 7)), (1, (2, 4, 7, 7)), (1, (3, 8, 14, 14))])
+def test_conv_split_equals_separate_convs(dt, pt_wide, shape):
     """fac_conv_nd_split over concatenated weights (S3D's merged Inception
-    heads) writes exactly what three separate fac_conv_nd launches write."""
-    from fac_fake_amd.ops import ConvLayer, conv_split
+    heads) writes exactly what three separate fac_conv_nd launches write:
+    on convnd_igemm (the default at this size) and on convnd_pt's column
+    segments (nd_pt_wide = 1: any row-tile count; 304 columns = two full
+    128-wide blocks and a partial one)."""
     g = torch.Generator().manual_seed(11)
-    n, d, h, w, cin, widths = 2, 4, 7, 7, 480, (192, 96, 16)
+    (n, d, h, w), cin, widths = shape, 480, (192, 96, 16)
+    _nd_pt_wide(pt_wide, dt)
+    try:
+        _split_case(g, n, d, h, w, cin, widths, dt)
+    finally:
+        _nd_pt_wide(1024, dt)
+
+
+def _split_case(g, n, d, h, w, cin, widths, dt):
+    from fac_fake_amd.ops import ConvLayer, conv_split
     x = torch.randn(n, d, h, w, cin, generator=g).to(T16[dt]).to(DEV)
     ws = [torch.randn(c, cin, 1, 1, 1, generator=g) / np.sqrt(cin) for c in widths]
     bs = [torch.randn(c, generator=g) * 0.1 for c in widths]
