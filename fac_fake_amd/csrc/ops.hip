@@ -2234,7 +2234,7 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
 // process-wide (fac_set_option "nd_pt_wide"): convnd_pt also for cout not a
 // multiple of 128 (a partial last column block) from this many 256-row tiles
 // on; 0 keeps those on convnd_igemm (A/B)
-static int g_nd_pt_wide = 1024;
+static int g_nd_pt_wide = 256;
 void set_nd_pt_wide(int v) { g_nd_pt_wide = v; }
 
 template <class T>
