@@ -24,6 +24,7 @@ namespace fac {
 int conv_block_n(int H, int cout);
 void set_conv_db(int v);
 void set_nd_pt_wide(int v);
+void set_pool_roll(int v);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
@@ -757,6 +758,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "nd_pt_wide") {  // convnd_pt for cout % 128 != 0 from this many 256-row tiles (default 256; 0: off); process-wide
     if (value < 0) return set_err(c, FAC_ERR_ARG, "nd_pt_wide must be >= 0");
     fac::set_nd_pt_wide(value);
+    return FAC_OK;
+  }
+  if (k == "pool_roll") {  // MaxPool3d(3,1,1) on 7-wide maps: 1 (default) maxpool3_roll, k >= 2 k frames per thread, 0 maxpool3_s1; process-wide
+    if (value < 0) return set_err(c, FAC_ERR_ARG, "pool_roll must be >= 0");
+    fac::set_pool_roll(value);
     return FAC_OK;
   }
   if (k == "stem_dynamic") {

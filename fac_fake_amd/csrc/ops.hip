@@ -545,6 +545,113 @@ __global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total, i
   }
 }
 
+// ---- maxpool3_roll (round 4): the same MaxPool3d(3, 1, 1) for 7-wide maps
+// (S3D's 4x7x7 Inception blocks), with three loads per output instead of
+// nine: 61.5-65.8 -> 33.6-35.2 us per call at 384 clips, bf16
+// (tools/pool_roll_ab.py; on the 8x14x14 maps the W = 14 instance was no
+// faster than maxpool3_s1 at 2 waves per SIMD: 200 / 300 vs 225 / 287 us).  One thread per (clip,
+// frame group, row y, 8-channel piece) walks a whole row of W positions
+// (compile time, fully unrolled) through the frames: per input frame the
+// three rows y-1..y+1 of each column are max-ed (3 loads per column), the
+// row's frame maxima F(x) = max over the 3 columns are rolled along x, and
+// the frame window along z: A = max(F(z-1), F(z)) and F(z) are kept packed
+// (16-bit, exact: a max selects one of its inputs) for the whole row, so
+// out(z) = max(A, F(z+1)).  Bit-identical to maxpool3_s1 up to the sign of
+// a zero (IEEE max of +0 and -0).  zg: output frames per thread.
+template <class T>
+__device__ __forceinline__ void max8(float (&m)[8], const u16x8 v) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], T::to_f32(v[i]));
+}
+template <class T>
+__device__ __forceinline__ u16x8 pack8(const float (&a)[8]) {
+  const u16x4 lo = T::pack4((f32x4){a[0], a[1], a[2], a[3]});
+  const u16x4 hi = T::pack4((f32x4){a[4], a[5], a[6], a[7]});
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <class T, int W>
+__global__ __launch_bounds__(256, W > 8 ? 2 : 3) void maxpool3_roll(fac_pool_desc p, int total, int zg) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int C = p.c, C8 = C / 8;
+  const int c8 = t % C8, t1 = t / C8;
+  const int y = t1 % p.h, t2 = t1 / p.h;
+  const int ngr = (p.d + zg - 1) / zg;
+  const int zgi = t2 % ngr, n = t2 / ngr;
+  const int z0 = zgi * zg, z1 = min(p.d, z0 + zg);
+  const size_t rs = (size_t)W * C, fs = (size_t)p.h * rs;
+  // rows y-1 / y+1 outside the map re-read row y (a max over a repeat)
+  const int ym = y > 0 ? y - 1 : y, yp = y + 1 < p.h ? y + 1 : y;
+  const uint16_t* inb = (const uint16_t*)p.in + (size_t)n * p.d * fs + c8 * 8;
+  // the row's frame maxima F(z, x), x = 0..W-1 in order, each handed to
+  // use(x, F) as soon as its three columns are in
+  auto frame = [&](int z, auto&& use) {
+    const uint16_t* f = inb + (size_t)z * fs;
+    float cm[8], cc[8], cn[8];  // column maxima x-2, x-1, x (rolled)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cm[i] = cc[i] = cn[i] = -__builtin_inff();
+#pragma unroll
+    for (int x = 0; x <= W; ++x) {
+      if (x < W) {
+        const u16x8 a = *(const u16x8*)(f + (size_t)ym * rs + (size_t)x * C);
+        const u16x8 b = *(const u16x8*)(f + (size_t)y * rs + (size_t)x * C);
+        const u16x8 c = *(const u16x8*)(f + (size_t)yp * rs + (size_t)x * C);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cn[i] = fmaxf(fmaxf(T::to_f32(a[i]), T::to_f32(b[i])), T::to_f32(c[i]));
+      }
+      if (x > 0) {
+        float m[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          m[i] = cc[i];
+          if (x > 1) m[i] = fmaxf(m[i], cm[i]);
+          if (x < W) m[i] = fmaxf(m[i], cn[i]);
+        }
+        use(x - 1, m);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        cm[i] = cc[i];
+        cc[i] = cn[i];
+      }
+    }
+  };
+  // A(x) = max(F(z-1, x), F(z, x)) and F(z, x), packed 16-bit (exact: a max
+  // selects one of its inputs)
+  u16x8 A[W], Fc[W];
+  frame(z0, [&](int x, const float (&m)[8]) { Fc[x] = A[x] = pack8<T>(m); });
+  if (z0 > 0)
+    frame(z0 - 1, [&](int x, const float (&m)[8]) {
+      float a[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = m[i];
+      max8<T>(a, Fc[x]);
+      A[x] = pack8<T>(a);
+    });
+  uint16_t* ob = (uint16_t*)p.out + ((size_t)n * p.d * p.h + (size_t)y) * W * p.ldo + p.c_off + c8 * 8;
+  const size_t ofs = (size_t)p.h * W * p.ldo;
+  for (int z = z0; z < z1; ++z) {
+    uint16_t* o = ob + (size_t)z * ofs;
+    if (z + 1 < p.d) {
+      frame(z + 1, [&](int x, const float (&m)[8]) {
+        float a[8], b[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a[i] = fmaxf(T::to_f32(A[x][i]), m[i]);
+          b[i] = fmaxf(T::to_f32(Fc[x][i]), m[i]);
+        }
+        *(u16x8*)(o + (size_t)x * p.ldo) = pack8<T>(a);
+        A[x] = pack8<T>(b);
+        Fc[x] = pack8<T>(m);
+      });
+    } else {
+#pragma unroll
+      for (int x = 0; x < W; ++x) *(u16x8*)(o + (size_t)x * p.ldo) = A[x];
+    }
+  }
+}
+
 // ---- input staging
 template <class T, bool U8>
 __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
@@ -2236,6 +2343,11 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
 // on; 0 keeps those on convnd_igemm (A/B)
 static int g_nd_pt_wide = 256;
 void set_nd_pt_wide(int v) { g_nd_pt_wide = v; }
+// process-wide (fac_set_option "pool_roll"): MaxPool3d(3,1,1) on 7-wide
+// maps by maxpool3_roll (1: every frame in one thread, k >= 2: k output
+// frames per thread), 0: maxpool3_s1 (A/B)
+static int g_pool_roll = 1;
+void set_pool_roll(int v) { g_pool_roll = v; }
 
 template <class T>
 static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
@@ -2724,6 +2836,17 @@ int fac_pool_nd(const fac_pool_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (d->mode == 0 && d->kd == 3 && d->kh == 3 && d->kw == 3 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
       d->pd == 1 && d->ph == 1 && d->pw == 1 && d->od == d->d && d->oh == d->h && d->ow == d->w) {
+    if (g_pool_roll && d->w == 7) {
+      const int zg = g_pool_roll == 1 ? d->d : std::min(g_pool_roll, d->d);
+      const long long rows = (long long)d->n * ((d->d + zg - 1) / zg) * d->h * (d->c / 8);
+      if (rows >= (1LL << 31)) return FAC_ERR_SHAPE;
+      const int nb = (int)((rows + 255) / 256);
+      if (d->dtype == FAC_DTYPE_BF16)
+        maxpool3_roll<BF16, 7><<<nb, 256, 0, st>>>(*d, (int)rows, zg);
+      else
+        maxpool3_roll<F16, 7><<<nb, 256, 0, st>>>(*d, (int)rows, zg);
+      return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+    }
     const int zg = d->d;  // output frames per thread: all of them
     const long long cols = (long long)d->n * ((d->d + zg - 1) / zg) * d->h * d->w * (d->c / 8);
     if (cols >= (1LL << 31)) return FAC_ERR_SHAPE;

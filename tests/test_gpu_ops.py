@@ -365,6 +365,35 @@ def test_max_pool_3x3x3_s1(dt, d):
     assert torch.equal(bc[..., 16:56], r) and bc[..., :16].abs().max() == 0 and bc[..., 56:].abs().max() == 0
 
 
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("d,h,roll", [(4, 7, 1), (1, 7, 1), (5, 3, 1), (6, 9, 4), (5, 7, 2), (4, 7, 0)])
+def test_max_pool_3x3x3_s1_roll(dt, d, h, roll):
+    """maxpool3_roll (MaxPool3d(3, 1, 1) on 7-wide maps, rolled along the row
+    and the frames; pool_roll 1 = every frame in one thread, k = k frames per
+    thread, 0 = maxpool3_s1): bit-exact vs torch, into a channel slot, for
+    maps shorter and taller than wide and frame counts not divisible by k."""
+    import ctypes
+    from fac_fake_amd import _lib
+    from fac_fake_amd.ops import pool
+    lib = _lib.load()
+    hd = ctypes.c_void_p()
+    _lib.check(lib.fac_create(0, _lib.DTYPES[dt], ctypes.byref(hd)), None, "fac_create")
+    g = torch.Generator().manual_seed(9 + d + h)
+    x = torch.randn(3, 48, d, h, 7, generator=g).to(T16[dt])
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV)
+    big = torch.zeros(3, d, h, 7, 64, dtype=T16[dt], device=DEV)
+    try:
+        _lib.check(lib.fac_set_option(hd, b"pool_roll", roll), hd, "fac_set_option")
+        pool(xg, 3, 1, 1, "max", out=big, c_off=8)
+        torch.cuda.synchronize()
+    finally:
+        lib.fac_set_option(hd, b"pool_roll", 1)
+        lib.fac_destroy(hd)
+    r = F.max_pool3d(x.float(), 3, 1, 1).permute(0, 2, 3, 4, 1)
+    bc = big.cpu().float()
+    assert torch.equal(bc[..., 8:56], r) and bc[..., :8].abs().max() == 0 and bc[..., 56:].abs().max() == 0
+
+
 def test_kan_linear_vs_reference(golden):
     from fac_fake_amd.ops import KANLinearLayer
     g = golden("resvitkan_golden.npz")
