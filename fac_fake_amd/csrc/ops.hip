@@ -474,6 +474,50 @@ __global__ __launch_bounds__(256) void pool_nd(fac_pool_desc p, int total) {
   *(u16x8*)((uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c8 * 8) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// ---- pool_max_win (round 4): max pooling with a compile-time window
+// (S3D's (1,3,3)/(1,2,2), (3,3,3)/2 and (2,2,2)/2, ResNet's 3x3/2), one
+// thread per (output position, 8-channel piece) as pool_nd, but branch-free:
+// taps outside the input re-read the nearest tap inside it (in floor mode
+// every window holds one, and a max over a repeat is unchanged), so all
+// KD*KH*KW loads issue together; pool_nd's per-tap bounds checks made each
+// load an exec-masked branch with its own wait.
+template <class T, int KD, int KH, int KW>
+__global__ __launch_bounds__(256) void pool_max_win(fac_pool_desc p, int total) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int C8 = p.c / 8;
+  const int c8 = t % C8, mo = t / C8;
+  const int ox = mo % p.ow, t1 = mo / p.ow;
+  const int oy = t1 % p.oh, t2 = t1 / p.oh;
+  const int oz = t2 % p.od, n = t2 / p.od;
+  const uint16_t* inb = (const uint16_t*)p.in + (size_t)n * p.d * p.h * p.w * p.c + c8 * 8;
+  int iz[KD], iy[KH], ix[KW];
+#pragma unroll
+  for (int k = 0; k < KD; ++k) iz[k] = min(max(oz * p.sd - p.pd + k, 0), p.d - 1);
+#pragma unroll
+  for (int k = 0; k < KH; ++k) iy[k] = min(max(oy * p.sh - p.ph + k, 0), p.h - 1);
+#pragma unroll
+  for (int k = 0; k < KW; ++k) ix[k] = min(max(ox * p.sw - p.pw + k, 0), p.w - 1);
+  u16x8 v[KD * KH * KW];
+#pragma unroll
+  for (int a = 0; a < KD; ++a)
+#pragma unroll
+    for (int b = 0; b < KH; ++b)
+#pragma unroll
+      for (int c = 0; c < KW; ++c)
+        v[(a * KH + b) * KW + c] = *(const u16x8*)(inb + (((size_t)iz[a] * p.h + iy[b]) * p.w + ix[c]) * p.c);
+  float m[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m[i] = -__builtin_inff();
+#pragma unroll
+  for (int k = 0; k < KD * KH * KW; ++k)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], T::to_f32(v[k][i]));
+  const u16x4 lo = T::pack4((f32x4){m[0], m[1], m[2], m[3]});
+  const u16x4 hi = T::pack4((f32x4){m[4], m[5], m[6], m[7]});
+  *(u16x8*)((uint16_t*)p.out + (size_t)mo * p.ldo + p.c_off + c8 * 8) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // ---- 3x3x3 / stride-1 / pad-1 max pooling (S3D's Inception branch3,
 // model.py:84-342: MaxPool3d(3, 1, 1) before the 1x1x1 conv): one thread per
 // (clip, position, 8-channel piece) walks the frames, taking each frame's
@@ -498,23 +542,22 @@ __global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total, i
   const int z0 = zgi * zg, z1 = min(p.d, z0 + zg);
   const size_t fs = (size_t)p.h * p.w * p.c;
   const uint16_t* inb = (const uint16_t*)p.in + (size_t)n * p.d * fs + c8 * 8;
+  // neighbours outside the map re-read the centre row / column (a max over
+  // a repeat): branch-free, so the nine loads issue together instead of one
+  // exec-masked load (and its wait) at a time
+  const int rows[3] = {y > 0 ? y - 1 : y, y, y + 1 < p.h ? y + 1 : y};
+  const int cols[3] = {x > 0 ? x - 1 : x, x, x + 1 < p.w ? x + 1 : x};
   auto frame_max = [&](int z, float (&m)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) m[i] = -__builtin_inff();
     const uint16_t* f = inb + (size_t)z * fs;
+    u16x8 v[9];
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int iy = y + dy;
-      if ((unsigned)iy >= (unsigned)p.h) continue;
+    for (int k = 0; k < 9; ++k) v[k] = *(const u16x8*)(f + ((size_t)rows[k / 3] * p.w + cols[k % 3]) * p.c);
 #pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int ix = x + dx;
-        if ((unsigned)ix >= (unsigned)p.w) continue;
-        const u16x8 v = *(const u16x8*)(f + ((size_t)iy * p.w + ix) * p.c);
+    for (int k = 0; k < 9; ++k)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], T::to_f32(v[i]));
-      }
-    }
+      for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], T::to_f32(v[k][i]));
   };
   float pm[8], cm[8], nm[8];
   if (z0 > 0) {
@@ -2348,6 +2391,10 @@ void set_nd_pt_wide(int v) { g_nd_pt_wide = v; }
 // frames per thread), 0: maxpool3_s1 (A/B)
 static int g_pool_roll = 1;
 void set_pool_roll(int v) { g_pool_roll = v; }
+// process-wide (fac_set_option "pool_win"): 1 (default) the strided max pools
+// with a compile-time window by pool_max_win, 0 pool_nd (A/B)
+static int g_pool_win = 1;
+void set_pool_win(int v) { g_pool_win = v; }
 
 template <class T>
 static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
@@ -2858,6 +2905,26 @@ int fac_pool_nd(const fac_pool_desc* d, void* stream) {
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   const int nb = (int)((total + 255) / 256);
+  // compile-time windows (branch-free taps) for the max pools of S3D / ResNet:
+  // floor-mode output dims and padding below the window keep a valid tap in
+  // every window (pool_nd takes anything else)
+  const bool floor_dims = d->od == (d->d + 2 * d->pd - d->kd) / d->sd + 1 &&
+                          d->oh == (d->h + 2 * d->ph - d->kh) / d->sh + 1 &&
+                          d->ow == (d->w + 2 * d->pw - d->kw) / d->sw + 1 && d->pd >= 0 && d->ph >= 0 &&
+                          d->pw >= 0 && d->pd < d->kd && d->ph < d->kh && d->pw < d->kw;
+  if (d->mode == 0 && g_pool_win && floor_dims) {
+    const bool bf = d->dtype == FAC_DTYPE_BF16;
+#define FAC_WIN(KD, KH, KW)                                                                                      \
+  if (d->kd == KD && d->kh == KH && d->kw == KW) {                                                            \
+    if (bf) pool_max_win<BF16, KD, KH, KW><<<nb, 256, 0, st>>>(*d, (int)total);                               \
+    else pool_max_win<F16, KD, KH, KW><<<nb, 256, 0, st>>>(*d, (int)total);                                   \
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;                                            \
+  }
+    FAC_WIN(1, 3, 3)
+    FAC_WIN(3, 3, 3)
+    FAC_WIN(2, 2, 2)
+#undef FAC_WIN
+  }
   if (d->dtype == FAC_DTYPE_BF16)
     pool_nd<BF16><<<nb, 256, 0, st>>>(*d, (int)total);
   else

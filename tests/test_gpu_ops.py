@@ -335,14 +335,19 @@ def test_pool_nd(dt):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(2, 24, 5, 17, 17, generator=g).to(T16[dt])
     xg = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV)
-    ym = pool(xg, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")
+    ym = pool(xg, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max")   # pool_max_win (compile-time windows)
     y3 = pool(xg, (3, 3, 3), (2, 2, 2), (1, 1, 1), "max")
+    y2 = pool(xg, 2, 2, 0, "max")
+    y5 = pool(xg, (1, 5, 3), (1, 3, 2), (0, 2, 1), "max")   # pool_nd (no compile-time window)
     ya = pool(xg, (2, 17, 17), (2, 17, 17), 0, "avg")
     torch.cuda.synchronize()
     rm = F.max_pool3d(x.float(), (1, 3, 3), (1, 2, 2), (0, 1, 1)).permute(0, 2, 3, 4, 1)
     r3 = F.max_pool3d(x.float(), 3, 2, 1).permute(0, 2, 3, 4, 1)
+    r2 = F.max_pool3d(x.float(), 2, 2).permute(0, 2, 3, 4, 1)
+    r5 = F.max_pool3d(x.float(), (1, 5, 3), (1, 3, 2), (0, 2, 1)).permute(0, 2, 3, 4, 1)
     ra = F.avg_pool3d(x.float(), (2, 17, 17)).permute(0, 2, 3, 4, 1)
     assert torch.equal(ym.cpu().float(), rm) and torch.equal(y3.cpu().float(), r3)
+    assert torch.equal(y2.cpu().float(), r2) and torch.equal(y5.cpu().float(), r5)
     assert _ulps(ya.cpu(), ra.to(T16[dt]), dt).max() <= 1.0
 
 

@@ -60,6 +60,22 @@ def main():
               + f"   {floor:6.1f}", flush=True)
         assert same
     print("total                         " + " ".join(f"{tot[v]:9.1f}" for v in arms), flush=True)
+    # the strided max pools of S3D's base (model.py:17-33): pool_nd (pool_win 0) vs pool_max_win (1)
+    print("strided pools: pool_win 0 / 1 (us), HBM floor", flush=True)
+    for d, hw, c, k, st, pd in ((8, 56, 64, (1, 3, 3), (1, 2, 2), (0, 1, 1)), (8, 28, 192, (1, 3, 3), (1, 2, 2), (0, 1, 1)),
+                                (8, 14, 480, 3, 2, 1), (4, 7, 832, 2, 2, 0)):
+        x = torch.randn(a.B, d, hw, hw, c, device=dev).relu().to(ops.TORCH16[a.dtype])
+        outs, us = {}, {}
+        for v in (0, 1):
+            _lib.check(lib.fac_set_option(h, b"pool_win", v), h, "fac_set_option")
+            outs[v] = ops.pool(x, k, st, pd, "max")
+            torch.cuda.synchronize()
+            us[v] = timed(lambda: ops.pool(x, k, st, pd, "max"), a.reps) * 1e3
+        same = torch.equal(outs[0], outs[1])
+        floor = (x.numel() + outs[0].numel()) * 2 / 8e12 * 1e6
+        print(f"{d}x{hw}x{hw}x{c:<4d} k{k} {'eq' if same else 'DIFF'} {us[0]:9.1f} {us[1]:9.1f}   {floor:6.1f}", flush=True)
+        assert same
+    _lib.check(lib.fac_set_option(h, b"pool_win", 1), h, "fac_set_option")
     _lib.check(lib.fac_set_option(h, b"pool_roll", 1), h, "fac_set_option")
     lib.fac_destroy(h)
 
