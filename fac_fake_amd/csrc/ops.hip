@@ -2395,6 +2395,10 @@ void set_pool_roll(int v) { g_pool_roll = v; }
 // with a compile-time window by pool_max_win, 0 pool_nd (A/B)
 static int g_pool_win = 1;
 void set_pool_win(int v) { g_pool_win = v; }
+// process-wide (fac_set_option "pool3_zg"): output frames per thread of
+// maxpool3_s1 (0: all, the default)
+static int g_pool3_zg = 0;
+void set_pool3_zg(int v) { g_pool3_zg = v; }
 
 template <class T>
 static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
@@ -2894,7 +2898,7 @@ int fac_pool_nd(const fac_pool_desc* d, void* stream) {
         maxpool3_roll<F16, 7><<<nb, 256, 0, st>>>(*d, (int)rows, zg);
       return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
     }
-    const int zg = d->d;  // output frames per thread: all of them
+    const int zg = g_pool3_zg > 0 ? std::min(g_pool3_zg, d->d) : d->d;  // output frames per thread (default all)
     const long long cols = (long long)d->n * ((d->d + zg - 1) / zg) * d->h * d->w * (d->c / 8);
     if (cols >= (1LL << 31)) return FAC_ERR_SHAPE;
     const int nb = (int)((cols + 255) / 256);

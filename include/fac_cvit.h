@@ -197,7 +197,16 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * outputs; process-wide, for A/B measurements), "fuse45" (1 = conv4 -> conv5
  * as one kernel, conv4 recomputed on each box's halo in LDS; 0 = two
  * launches, the default: the fused kernel measured neutral, DESIGN.md §3.4;
- * bit-identical outputs). */
+ * bit-identical outputs).  Process-wide knobs of the fac_ops.h layer kernels
+ * (A/B measurements; any context sets them): "nd_pt_wide" (n >= 0: convnd_pt
+ * also takes uniform-tap convs whose cout is not a multiple of 128, and
+ * fac_conv_nd_split's column segments, from n 256-row tiles on; default 256,
+ * 0 = convnd_igemm), "pool_roll" (MaxPool3d(3,1,1) on 7-wide maps by
+ * maxpool3_roll: 1 = every frame in one thread, the default; k >= 2 = k frames
+ * per thread; 0 = maxpool3_s1), "pool3_zg" (output frames per thread of
+ * maxpool3_s1, 0 = all, the default), "pool_win" (1 = the (1,3,3) / (3,3,3) /
+ * (2,2,2) max pools by the compile-time-window kernel, the default; 0 =
+ * pool_nd); every setting gives bit-identical max pools. */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);
