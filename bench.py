@@ -252,10 +252,11 @@ def layer_roofline_ms(run, dtype: str) -> dict:
 
     orig_s2dc = ops.conv_s2d4_clip
 
-    def s2dc_hook(layer, clip, **kw):   # S3D's first conv with the s2d packing folded in: fp32 clip in
+    def s2dc_hook(layer, clip, **kw):   # S3D's first conv with the s2d packing folded in: fp32 / uint8 clip in
         out = orig_s2dc(layer, clip, **kw)
         M = out.numel() // layer.cout
-        recs.append((2.0 * M * layer.cout * layer.g.kh * layer.g.kw * layer.cin, 4.0 * clip.numel() + 2.0 * out.numel()))
+        recs.append((2.0 * M * layer.cout * layer.g.kh * layer.g.kw * layer.cin,
+                     clip.element_size() * clip.numel() + 2.0 * out.numel()))
         return out
 
     orig_dual = ops.conv_dual
@@ -379,7 +380,9 @@ def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, w
     from fac_fake_amd.weights import make_s3d_state_dict, s3d_clips
     m = S3D(1, srm, dtype=dtype)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, srm == "yes").items()})
-    x = torch.from_numpy(s3d_clips(B, 16, 112, seed=50 + int(os.environ.get("RANK", "0")))).to(dev)
+    # the clips as decoded frames (uint8: S3D-test.py:94-96's values before its
+    # float cast, bit-identical logits to the fp32 clip, a quarter of the bytes)
+    x = torch.from_numpy(s3d_clips(B, 16, 112, seed=50 + int(os.environ.get("RANK", "0")))).to(torch.uint8).to(dev)
     s = torch.cuda.Stream(dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
@@ -408,7 +411,8 @@ def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, w
         lr = layer_roofline_ms(lambda: m(x), dtype)
     ms = el / steps * 1e3
     lr["fraction_of_step"] = round(lr["roofline_ms"] / ms, 4)
-    return {"workload": f"config 4: S3D forward (SRM_net={srm}), B={B} raw 16x112x112 clips per GPU, hipGraph per step",
+    return {"workload": f"config 4: S3D forward (SRM_net={srm}), B={B} raw uint8 16x112x112 clips per GPU, "
+                        "hipGraph per step",
             "value": round(v, 1), "unit": "clips/s", "n_gpus": world, "ms_per_step": round(ms, 3),
             "dtype": dtype,
             "mfma_roofline_fraction": round(v * S3D_FLOP_PER_CLIP / (world * PEAK_TFLOPS[dtype] * 1e12), 4),

@@ -24,6 +24,7 @@
 // contiguous burst.
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -954,7 +955,10 @@ __global__ __launch_bounds__(256) void sigmoid_k(const float* __restrict__ x, fl
 // of a cell: 2 pixels x 3 channels + 2 zeros) into registers one box ahead,
 // and converted + written to the other halo buffer after this box's MFMAs
 // and stores; plain loads only, so the compiler's vmcnt waits are exact.
-template <class T, bool F32IN = false>
+// IN: 0 = fac_pack_input_s2d cells, 1 = the fp32 clip (F32IN above), 2 = a
+// uint8 clip (decoded video frames, the same 0..255 values a quarter of the
+// bytes: one 2-byte pixel pair per colour plane, widened at the cell write).
+template <class T, int IN = 0>
 __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_, const uint16_t* __restrict__ w,
                                                     const float* __restrict__ bias, uint16_t* __restrict__ out,
                                                     int nbox, int Hc, int Wc, int Ho, int Wo, int kp, int relu_on,
@@ -1015,12 +1019,14 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
   // F32IN: this lane's cell pieces p = tid + 256 j of the dense 2 x 11 x 31
   // halo (piece 0 / 1 = the cell's top / bottom pixel row), as raw float pairs
   constexpr int NPC = 2 * HH * HWD, PPL = (NPC + 255) / 256;
-  float2 raw[F32IN ? PPL : 1][3];
+  constexpr bool F32IN = IN != 0;  // the cells are made from a raw clip while staging
+  using RawT = typename std::conditional<IN == 2, uint16_t, float2>::type;
+  RawT raw[F32IN ? PPL : 1][3];
   auto load_raw = [&](int bx) {
     const int img = bx / bpi, rr = bx - img * bpi;
     const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
     const int clip = img / frames, f = img - clip * frames;
-    const float* src = (const float*)in_ + (size_t)clip * 3 * frames * H * W + (size_t)f * H * W;
+    const size_t cbase = (size_t)clip * 3 * frames * H * W + (size_t)f * H * W;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int p = tid + 256 * j;
@@ -1030,8 +1036,13 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
       const size_t off = ok ? (size_t)y * W + x : 0;  // branch-free: masked pieces read pixel 0 and are zeroed
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const float2 v = *(const float2*)(src + (size_t)c * frames * H * W + off);
-        raw[j][c] = ok ? v : make_float2(0.f, 0.f);
+        if constexpr (IN == 2) {
+          const uint16_t v = *(const uint16_t*)((const uint8_t*)in_ + cbase + (size_t)c * frames * H * W + off);
+          raw[j][c] = ok ? v : (uint16_t)0;
+        } else {
+          const float2 v = *(const float2*)((const float*)in_ + cbase + (size_t)c * frames * H * W + off);
+          raw[j][c] = ok ? v : make_float2(0.f, 0.f);
+        }
       }
     }
   };
@@ -1041,14 +1052,22 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
       const int p = tid + 256 * j;
       if (p < NPC) {
         const int pc = p / (HH * HWD), rem = p - pc * (HH * HWD), hy = rem / HWD, hx = rem - (rem / HWD) * HWD;
+        float2 rf[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          if constexpr (IN == 2)
+            rf[c] = make_float2((float)(raw[j][c] & 0xff), (float)(raw[j][c] >> 8));  // little-endian pixel pair
+          else
+            rf[c] = raw[j][c];
+        }
         u16x8 v;
-        v[0] = T::from_f32(raw[j][0].x);
-        v[1] = T::from_f32(raw[j][1].x);
-        v[2] = T::from_f32(raw[j][2].x);
+        v[0] = T::from_f32(rf[0].x);
+        v[1] = T::from_f32(rf[1].x);
+        v[2] = T::from_f32(rf[2].x);
         v[3] = 0;
-        v[4] = T::from_f32(raw[j][0].y);
-        v[5] = T::from_f32(raw[j][1].y);
-        v[6] = T::from_f32(raw[j][2].y);
+        v[4] = T::from_f32(rf[0].y);
+        v[5] = T::from_f32(rf[1].y);
+        v[6] = T::from_f32(rf[2].y);
         v[7] = 0;
         *(u16x8*)(halo + ((pc * HH + hy) * RPX + hx) * 8) = v;
       }
@@ -2702,7 +2721,8 @@ int fac_conv_nd(const fac_conv_desc* d, void* stream) {
   return conv_nd_impl(d, nullptr, 0, INT_MAX, nullptr, 0, INT_MAX, stream);
 }
 
-int fac_conv_s2d4_clip(const fac_conv_desc* d, const float* clip, int h, int w, int pad_before, void* stream) {
+static int conv_s2d4_clip_impl(const fac_conv_desc* d, const void* clip, bool u8, int h, int w, int pad_before,
+                               void* stream) {
   using namespace fac;
   if (!d || !clip || !d->weight || !d->out || (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16))
     return FAC_ERR_ARG;
@@ -2728,13 +2748,21 @@ int fac_conv_s2d4_clip(const fac_conv_desc* d, const float* clip, int h, int w, 
   const int grid = std::min(nbox, 2 * ncu);
   const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
   hipStream_t st = (hipStream_t)stream;
-  if (d->dtype == FAC_DTYPE_BF16)
-    conv_s2d4<BF16, true><<<grid, 256, 0, st>>>(clip, (const uint16_t*)d->weight, d->bias, (uint16_t*)d->out, nbox,
-                                                d->h, d->w, d->oh, d->ow, k_pad, relu_on, d->d, h, w, pad_before);
-  else
-    conv_s2d4<F16, true><<<grid, 256, 0, st>>>(clip, (const uint16_t*)d->weight, d->bias, (uint16_t*)d->out, nbox,
-                                               d->h, d->w, d->oh, d->ow, k_pad, relu_on, d->d, h, w, pad_before);
+#define FAC_S2DC(TT, IN)                                                                                          \
+  conv_s2d4<TT, IN><<<grid, 256, 0, st>>>(clip, (const uint16_t*)d->weight, d->bias, (uint16_t*)d->out, nbox, d->h, \
+                                          d->w, d->oh, d->ow, k_pad, relu_on, d->d, h, w, pad_before)
+  if (d->dtype == FAC_DTYPE_BF16) u8 ? FAC_S2DC(BF16, 2) : FAC_S2DC(BF16, 1);
+  else u8 ? FAC_S2DC(F16, 2) : FAC_S2DC(F16, 1);
+#undef FAC_S2DC
   return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_conv_s2d4_clip(const fac_conv_desc* d, const float* clip, int h, int w, int pad_before, void* stream) {
+  return conv_s2d4_clip_impl(d, clip, false, h, w, pad_before, stream);
+}
+
+int fac_conv_s2d4_clip_u8(const fac_conv_desc* d, const uint8_t* clip, int h, int w, int pad_before, void* stream) {
+  return conv_s2d4_clip_impl(d, clip, true, h, w, pad_before, stream);
 }
 
 int fac_conv_nd_split(const fac_conv_desc* d, void* out1, int ldo1, int split1, void* out2, int ldo2, int split2,

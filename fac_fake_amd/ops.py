@@ -407,10 +407,12 @@ def conv_s2d4_clip(layer: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2,
     launch (fac_conv_s2d4_clip): S3D's base.0 spatial (1,7,7)/(1,2,2) conv
     (model.py:18) with the space-to-depth packing folded into the conv's halo
     staging, so the 16-bit cell image never goes through HBM.  ``clip`` is the
-    fp32 batch [N, 3, T, h, w]; ``layer`` the s2d-weight 4x4 conv.
-    Bit-identical to the two launches."""
-    if clip.dtype != torch.float32 or clip.dim() != 5 or clip.shape[1] != 3 or not clip.is_contiguous():
-        raise ValueError(f"expected a contiguous fp32 clip [N,3,T,H,W], got {clip.dtype} {tuple(clip.shape)}")
+    fp32 batch [N, 3, T, h, w], or uint8 (fac_conv_s2d4_clip_u8: decoded
+    frames, a quarter of the bytes, the output of the same clip cast to fp32);
+    ``layer`` the s2d-weight 4x4 conv.  Bit-identical to the two launches."""
+    if clip.dtype not in (torch.float32, torch.uint8) or clip.dim() != 5 or clip.shape[1] != 3 or \
+            not clip.is_contiguous():
+        raise ValueError(f"expected a contiguous fp32 / uint8 clip [N,3,T,H,W], got {clip.dtype} {tuple(clip.shape)}")
     n, _, t, h, w = clip.shape
     hc, wc = h // 2 + pad_before + pad_after, w // 2 + pad_before + pad_after
     od, oh, ow = layer.out_dims(t, hc, wc)
@@ -426,8 +428,8 @@ def conv_s2d4_clip(layer: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2,
     dsc.od, dsc.oh, dsc.ow = od, oh, ow
     dsc.out, dsc.ldo, dsc.c_off = out.data_ptr(), layer.cout, 0
     dsc.flags = RELU if relu else 0
-    _lib.check(_lib.load().fac_conv_s2d4_clip(ctypes.byref(dsc), clip.data_ptr(), h, w, pad_before, _stream(clip)),
-               None, "fac_conv_s2d4_clip")
+    fn = "fac_conv_s2d4_clip_u8" if clip.dtype == torch.uint8 else "fac_conv_s2d4_clip"
+    _lib.check(getattr(_lib.load(), fn)(ctypes.byref(dsc), clip.data_ptr(), h, w, pad_before, _stream(clip)), None, fn)
     return out
 
 

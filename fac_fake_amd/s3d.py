@@ -249,7 +249,7 @@ class S3D(nn.Module):
                 # the raw fp32 clip (`_pack`): the space-to-depth packing runs
                 # inside the conv's halo staging (ops.conv_s2d4_clip); packed
                 # cells (ops.pack_input_s2d) still take the plain conv
-                y = L[1](ops.conv_s2d4_clip(L[0], y) if y.dtype == torch.float32 else L[0](y))
+                y = L[1](ops.conv_s2d4_clip(L[0], y) if y.dtype in (torch.float32, torch.uint8) else L[0](y))
             elif kind == "sep":
                 y = L[1](L[0](y))
             elif kind == "basic":
@@ -271,7 +271,11 @@ class S3D(nn.Module):
         _, _, T, H, W = x.shape
         if self._srm:
             return pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
-        # base.0's space-to-depth cells are made inside its conv (ops.conv_s2d4_clip)
+        # base.0's space-to-depth cells are made inside its conv (ops.conv_s2d4_clip);
+        # a uint8 clip (decoded frames: the reference's values before its float
+        # cast, S3D-test.py:94-96) is read as is, a quarter of the bytes
+        if x.dtype == torch.uint8 and _lib.exports("fac_conv_s2d4_clip_u8"):
+            return x.contiguous()
         if _lib.exports("fac_conv_s2d4_clip"):
             return x.float().contiguous()
         return pack_input_s2d(x.float(), dtype=self.dtype_name, u8=False, pad_before=2, pad_after=1)

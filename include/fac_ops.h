@@ -168,6 +168,13 @@ int fac_pack_input_s2d(int dtype, const void* src, int src_kind, int n, int fram
  * is bit-identical to fac_pack_input_s2d + fac_conv_nd. */
 int fac_conv_s2d4_clip(const fac_conv_desc* desc, const float* clip, int h, int w, int pad_before, void* stream);
 
+/* fac_conv_s2d4_clip over a uint8 clip batch [n][3][frames][h][w] (decoded
+ * video frames, S3D-test.py:94-96's 0..255 values before the float cast): the
+ * same output as fac_conv_s2d4_clip on that clip cast to fp32, a quarter of
+ * the input bytes.  Round-4 addition, no reference counterpart. */
+int fac_conv_s2d4_clip_u8(const fac_conv_desc* desc, const uint8_t* clip, int h, int w, int pad_before,
+                          void* stream);
+
 /* KANLinear forward (CViT-main/ResVitKan/kan.py:189-206), fp32:
  *   y = silu(x) · base_weightᵀ + b_splines(x) · (spline_weight ⊙ spline_scaler)ᵀ
  * with order-3 B-spline bases over the per-feature knot vector `grid`

@@ -206,6 +206,12 @@ def test_conv_s2d4_clip_equals_pack_then_conv(n, t, relu, dt):
     torch.cuda.synchronize()
     assert tuple(fused.shape) == (n, t, 56, 56, 64)
     assert torch.equal(fused.view(torch.int16).cpu(), ref.view(torch.int16).cpu())
+    # the uint8 clip (fac_conv_s2d4_clip_u8) equals the fp32 path on the same values
+    clip8 = clip.to(torch.uint8)
+    f8 = conv_s2d4_clip(layer, clip8, relu=relu)
+    f32 = conv_s2d4_clip(layer, clip8.float(), relu=relu)
+    torch.cuda.synchronize()
+    assert torch.equal(f8.view(torch.int16).cpu(), f32.view(torch.int16).cpu())
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
@@ -523,10 +529,12 @@ def test_s3d_matches_reference(s3d_models, golden, srm, dt, tol16):
     g = golden("s3d_golden.npz")
     x = torch.from_numpy(s3d_clips(2, 16, 112, seed=int(g["clip_seed"]))).to(DEV)
     lg, pr = s3d_models[(srm, dt)](x, return_probs=True)
+    lg8 = s3d_models[(srm, dt)](x.to(torch.uint8))   # decoded-frame input: the same integer values
     torch.cuda.synchronize()
     p_ref = 1 / (1 + np.exp(-g[f"logits_{srm}"].astype(np.float64)))
     assert lg.shape == (2, 1)
     assert np.abs(pr.cpu().numpy() - p_ref).max() <= tol
+    assert torch.equal(lg8, lg)
 
 
 @pytest.mark.parametrize("srm", ["no", "yes"])
