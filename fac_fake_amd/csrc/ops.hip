@@ -696,6 +696,109 @@ __global__ __launch_bounds__(256, W > 8 ? 2 : 3) void maxpool3_roll(fac_pool_des
   }
 }
 
+// ---- maxpool3_lds14 (round 4): MaxPool3d(3, 1, 1) on 14 x 14 maps (S3D's
+// Mixed_3b / 3c branch3 at 112^2 clips).  maxpool3_s1 reads each input nine
+// times through L1, which the ~20 resident waves of a CU thrash (0.25 of the
+// HBM rate).  Here one workgroup per (clip, 64-channel slice) walks the
+// frames: each frame's 14 x 14 x 64 slice is read from HBM once into an LDS
+// image with a -inf border (16 x 16 cells of 8 x 16 bytes, double-buffered,
+// the next frame prefetched into registers behind the current one's
+// arithmetic), every position's 3 x 3 frame maximum comes from LDS, and the
+// window over the frames is rolled in registers (A = max(F(z-1), F(z)),
+// F(z), packed 16-bit: a max selects one of its inputs).  Bit-identical to
+// maxpool3_s1 up to the sign of a zero.
+template <class T>
+__global__ __launch_bounds__(256) void maxpool3_lds14(fac_pool_desc p) {
+  constexpr int S = 14, B = 16, NIT = (S * S * 8 + 255) / 256;  // 1568 items (position, piece): 7 per thread
+  __shared__ __attribute__((aligned(16))) uint16_t img[2][B * B * 8 * 8];
+  const int tid = threadIdx.x;
+  const int nsl = p.c / 64, n = blockIdx.x / nsl, cs = blockIdx.x - n * nsl;
+  // the -inf border of both images (the interior is rewritten every frame)
+  const uint16_t ninf = T::from_f32(-__builtin_inff());
+  for (int q = tid; q < 2 * B * B * 8; q += 256) {
+    const int b = q / (B * B * 8), r = q - b * (B * B * 8), cell = r / 8, hy = cell / B, hx = cell - hy * B;
+    if (hy == 0 || hy == B - 1 || hx == 0 || hx == B - 1) {
+      u16x8 v;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = ninf;
+      *(u16x8*)(img[b] + r * 8) = v;
+    }
+  }
+  const size_t fs = (size_t)S * S * p.c;
+  const uint16_t* inb = (const uint16_t*)p.in + (size_t)n * p.d * fs + cs * 64;
+  int gof[NIT], lof[NIT];  // per item: global element offset in a frame, LDS element offset of its centre
+  bool val[NIT];
+#pragma unroll
+  for (int j = 0; j < NIT; ++j) {
+    const int q = tid + 256 * j, px = q / 8, c8 = q - px * 8, y = px / S, x = px - y * S;
+    val[j] = q < S * S * 8;
+    gof[j] = val[j] ? px * p.c + c8 * 8 : 0;
+    lof[j] = (((y + 1) * B + x + 1) * 8 + c8) * 8;
+  }
+  u16x8 pre[NIT];
+  auto load = [&](int z) {
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) pre[j] = *(const u16x8*)(inb + (size_t)z * fs + gof[j]);
+  };
+  auto put = [&](int b) {
+#pragma unroll
+    for (int j = 0; j < NIT; ++j)
+      if (val[j]) *(u16x8*)(img[b] + lof[j]) = pre[j];
+  };
+  // F(z) of item j from image b: the 3 x 3 max around its centre
+  auto fmax9 = [&](int b, int j, float (&m)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) m[i] = -__builtin_inff();
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) max8<T>(m, *(const u16x8*)(img[b] + lof[j] + (dy * B + dx) * 64));
+  };
+  u16x8 A[NIT], Fc[NIT];
+  load(0);
+  put(0);
+  __syncthreads();
+  if (p.d > 1) load(1);
+#pragma unroll
+  for (int j = 0; j < NIT; ++j) {
+    float m[8];
+    fmax9(0, j, m);
+    Fc[j] = A[j] = pack8<T>(m);
+  }
+  uint16_t* ob = (uint16_t*)p.out + (size_t)n * p.d * S * S * p.ldo + p.c_off + cs * 64;
+  for (int z = 0; z < p.d; ++z) {
+    uint16_t* o = ob + (size_t)z * S * S * p.ldo;
+    if (z + 1 < p.d) {
+      const int b = (z + 1) & 1;
+      put(b);
+      __syncthreads();
+      if (z + 2 < p.d) load(z + 2);
+#pragma unroll
+      for (int j = 0; j < NIT; ++j) {
+        if (!val[j]) continue;
+        float m[8], a[8], c[8];
+        fmax9(b, j, m);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a[i] = fmaxf(T::to_f32(A[j][i]), m[i]);
+          c[i] = fmaxf(T::to_f32(Fc[j][i]), m[i]);
+        }
+        const int q = tid + 256 * j, px = q / 8, c8 = q - px * 8;
+        *(u16x8*)(o + (size_t)px * p.ldo + c8 * 8) = pack8<T>(a);
+        A[j] = pack8<T>(c);
+        Fc[j] = pack8<T>(m);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NIT; ++j) {
+        if (!val[j]) continue;
+        const int q = tid + 256 * j, px = q / 8, c8 = q - px * 8;
+        *(u16x8*)(o + (size_t)px * p.ldo + c8 * 8) = A[j];
+      }
+    }
+  }
+}
+
 // ---- input staging
 template <class T, bool U8>
 __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
@@ -2418,6 +2521,10 @@ void set_pool_win(int v) { g_pool_win = v; }
 // maxpool3_s1 (0: all, the default)
 static int g_pool3_zg = 0;
 void set_pool3_zg(int v) { g_pool3_zg = v; }
+// process-wide (fac_set_option "pool_lds14"): 1 (default) MaxPool3d(3,1,1) on
+// 14 x 14 maps with 64-multiple channels by maxpool3_lds14, 0 maxpool3_s1
+static int g_pool_lds14 = 1;
+void set_pool_lds14(int v) { g_pool_lds14 = v; }
 
 template <class T>
 static bool launch_convnd_pt(ConvP& p, hipStream_t st) {
@@ -2915,6 +3022,15 @@ int fac_pool_nd(const fac_pool_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (d->mode == 0 && d->kd == 3 && d->kh == 3 && d->kw == 3 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
       d->pd == 1 && d->ph == 1 && d->pw == 1 && d->od == d->d && d->oh == d->h && d->ow == d->w) {
+    if (g_pool_lds14 && d->h == 14 && d->w == 14 && d->c % 64 == 0 && d->ldo % 8 == 0) {
+      const long long nwg = (long long)d->n * (d->c / 64);
+      if (nwg >= (1LL << 31)) return FAC_ERR_SHAPE;
+      if (d->dtype == FAC_DTYPE_BF16)
+        maxpool3_lds14<BF16><<<(int)nwg, 256, 0, st>>>(*d);
+      else
+        maxpool3_lds14<F16><<<(int)nwg, 256, 0, st>>>(*d);
+      return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+    }
     if (g_pool_roll && d->w == 7) {
       const int zg = g_pool_roll == 1 ? d->d : std::min(g_pool_roll, d->d);
       const long long rows = (long long)d->n * ((d->d + zg - 1) / zg) * d->h * (d->c / 8);

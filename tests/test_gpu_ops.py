@@ -405,6 +405,25 @@ def test_max_pool_3x3x3_s1_roll(dt, d, h, roll):
     assert torch.equal(bc[..., 8:56], r) and bc[..., :8].abs().max() == 0 and bc[..., 56:].abs().max() == 0
 
 
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("d,c", [(1, 64), (2, 128), (5, 192), (8, 64)])
+def test_max_pool_3x3x3_s1_lds14(dt, d, c):
+    """maxpool3_lds14 (MaxPool3d(3, 1, 1) on 14x14 maps: one workgroup per
+    (clip, 64-channel slice), frames through a -inf-bordered LDS image, the
+    frame window rolled in registers): bit-exact vs torch into a channel slot
+    of a wider tensor, for 1..8 frames and 1..3 channel slices."""
+    from fac_fake_amd.ops import pool
+    g = torch.Generator().manual_seed(21 + d + c)
+    x = torch.randn(3, c, d, 14, 14, generator=g).to(T16[dt])
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV)
+    big = torch.zeros(3, d, 14, 14, c + 16, dtype=T16[dt], device=DEV)
+    pool(xg, 3, 1, 1, "max", out=big, c_off=8)
+    torch.cuda.synchronize()
+    r = F.max_pool3d(x.float(), 3, 1, 1).permute(0, 2, 3, 4, 1)
+    bc = big.cpu().float()
+    assert torch.equal(bc[..., 8:8 + c], r) and bc[..., :8].abs().max() == 0 and bc[..., 8 + c:].abs().max() == 0
+
+
 def test_kan_linear_vs_reference(golden):
     from fac_fake_amd.ops import KANLinearLayer
     g = golden("resvitkan_golden.npz")

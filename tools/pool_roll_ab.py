@@ -60,6 +60,21 @@ def main():
               + f"   {floor:6.1f}", flush=True)
         assert same
     print("total                         " + " ".join(f"{tot[v]:9.1f}" for v in arms), flush=True)
+    # maxpool3_lds14 (pool_lds14 1) vs maxpool3_s1 (0) on the 14x14 maps
+    print("14x14 maps: pool_lds14 0 / 1 (us), HBM floor", flush=True)
+    for d, hw, c in ((8, 14, 192), (8, 14, 256), (3, 14, 64)):
+        x = torch.randn(a.B, d, hw, hw, c, device=dev).relu().to(ops.TORCH16[a.dtype])
+        outs, us = {}, {}
+        for v in (0, 1):
+            _lib.check(lib.fac_set_option(h, b"pool_lds14", v), h, "fac_set_option")
+            outs[v] = ops.pool(x, 3, 1, 1, "max")
+            torch.cuda.synchronize()
+            us[v] = timed(lambda: ops.pool(x, 3, 1, 1, "max"), a.reps) * 1e3
+        same = torch.equal(outs[0], outs[1])
+        floor = 2 * x.numel() * 2 / 8e12 * 1e6
+        print(f"{d}x{hw}x{hw}x{c:<4d} {'eq' if same else 'DIFF'} {us[0]:9.1f} {us[1]:9.1f}   {floor:6.1f}", flush=True)
+        assert same
+    _lib.check(lib.fac_set_option(h, b"pool_lds14", 0), h, "fac_set_option")
     # maxpool3_s1's output frames per thread on the 14x14 maps (pool3_zg; 0 = all)
     print("maxpool3_s1 frames per thread: pool3_zg 0 / 1 / 2 / 4 (us)", flush=True)
     for d, hw, c in ((8, 14, 192), (8, 14, 256)):
@@ -74,6 +89,7 @@ def main():
         print(f"{d}x{hw}x{hw}x{c:<4d} {'eq' if same else 'DIFF'} " + " ".join(f"{us[v]:9.1f}" for v in (0, 1, 2, 4)), flush=True)
         assert same
     _lib.check(lib.fac_set_option(h, b"pool3_zg", 0), h, "fac_set_option")
+    _lib.check(lib.fac_set_option(h, b"pool_lds14", 1), h, "fac_set_option")
     # the strided max pools of S3D's base (model.py:17-33): pool_nd (pool_win 0) vs pool_max_win (1)
     print("strided pools: pool_win 0 / 1 (us), HBM floor", flush=True)
     for d, hw, c, k, st, pd in ((8, 56, 64, (1, 3, 3), (1, 2, 2), (0, 1, 1)), (8, 28, 192, (1, 3, 3), (1, 2, 2), (0, 1, 1)),
