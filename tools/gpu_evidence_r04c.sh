@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-4 evidence pass c (late round): every GPU test, smoke, the default
+# bench line, then the config-2 kernel trace + PMC passes (tools/profile_r04.sh,
+# PROF_TAG=c).  Configs 4/5: tools/gpu_evidence_r04c_cfg45.sh.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -rA > gpurun_out/pytest_gpu.log 2>&1 || { grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head -20; tail -5 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -5 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 600 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -5 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log | cut -c1-300
+[ -n "$NO_PROF" ] && exit 0
+PROF_TAG=c bash tools/profile_r04.sh || exit 1
