@@ -491,8 +491,11 @@ def main():
     ap.add_argument("--no-s3d", action="store_true", help="skip the config-4 S3D sub-measurement")
     ap.add_argument("--no-repbn8", action="store_true", help="skip the RepBn8-variant sub-measurement")
     ap.add_argument("--only", choices=["resvitkan", "s3d", "repbn8"], help="run only one sub-measurement (profiling)")
-    ap.add_argument("--s3d-batch", type=int, default=384, help="clips per step of the config-4 S3D measurement")
-    ap.add_argument("--rvk-batch", type=int, default=1024, help="crops per step of the config-5 ResVitKan measurement")
+    # per-GPU batches of the configs-4/5 sub-measurements (the configs leave them
+    # open; late round-4 sweep, profiles/r04_batch_sweep*.txt: S3D 384 -> 1536
+    # clips +13 %, ResVitKan 1024 -> 3072 crops +7 %)
+    ap.add_argument("--s3d-batch", type=int, default=1536, help="clips per step of the config-4 S3D measurement")
+    ap.add_argument("--rvk-batch", type=int, default=3072, help="crops per step of the config-5 ResVitKan measurement")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="fac_set_option knob (include/fac_cvit.h), repeatable")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
