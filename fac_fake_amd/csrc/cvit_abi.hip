@@ -24,6 +24,7 @@ namespace fac {
 int conv_block_n(int H, int cout);
 void set_conv_db(int v);
 void set_nd_pt_wide(int v);
+void set_nd_occ3(int v);
 void set_pool_roll(int v);
 void set_pool_win(int v);
 void set_pool3_zg(int v);
@@ -756,6 +757,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   }
   if (k == "conv_db") {  // 1 (default): conv3x3_db for the 28^2 tiles; 0: the LDS weight ring (A/B); process-wide
     fac::set_conv_db(value);
+    return FAC_OK;
+  }
+  if (k == "nd_occ3") {  // convnd_igemm 3-per-CU tile for cout <= 64 up to this many K steps (default 4; 0 = off); process-wide
+    if (value < 0) return set_err(c, FAC_ERR_ARG, "nd_occ3 must be >= 0");
+    fac::set_nd_occ3(value);
     return FAC_OK;
   }
   if (k == "nd_pt_wide") {  // convnd_pt for cout % 128 != 0 from this many 256-row tiles (default 256; 0: off); process-wide

@@ -2508,6 +2508,11 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
 // on; 0 keeps those on convnd_igemm (A/B)
 static int g_nd_pt_wide = 256;
 void set_nd_pt_wide(int v) { g_nd_pt_wide = v; }
+// process-wide (fac_set_option "nd_occ3"): convnd_igemm's 3-per-CU 2-slot
+// 128 x 64 tile also for cout <= 64 up to this many K steps (default 4: S3D's
+// narrow SepConv halves, config 4 +0.3 to +0.6 %; 0: K <= 128 only)
+static int g_nd_occ3 = 4;
+void set_nd_occ3(int v) { g_nd_occ3 = v; }
 // process-wide (fac_set_option "pool_roll"): MaxPool3d(3,1,1) on 7-wide
 // maps by maxpool3_roll (1: every frame in one thread, k >= 2: k output
 // frames per thread), 0: maxpool3_s1 (A/B)
@@ -2566,7 +2571,7 @@ static void launch_convnd_t(ConvP p, hipStream_t st) {
   const int gx64 = (p.M + 63) / 64, gx128 = (p.M + 127) / 128, gx256 = (p.M + 255) / 256;
   const int ny64 = (p.Cout + 63) / 64, ny128 = (p.Cout + 127) / 128;
   constexpr int nd256_min = 256;  // 256 x 128 tiles only when they fill the chip at least once
-  if (p.ksteps <= 2) {
+  if (p.ksteps <= 2 || (g_nd_occ3 && p.Cout <= 64 && p.ksteps <= g_nd_occ3)) {
     // K <= 128 (1x1 expansions): memory-bound, so occupancy first — a 2-slot
     // ring (48 KB) lets three 128 x 64 workgroups share a CU
     const dim3 g = conv_grid(p, gx128, ny64);
