@@ -845,20 +845,31 @@ __global__ __launch_bounds__(256) void pack_input_s2d(const void* src, int n_img
   const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
   u16x8 lo = (u16x8)0, hi = (u16x8)0;
   const int y0 = 2 * (Y - pb), x0 = 2 * (X - pb);
+  // branch-free: out-of-image pixels load pixel 0 and are zeroed, so the 12
+  // loads issue together (one exec-masked branch per pixel made each wait)
+  float v[4][3];
+  bool ok[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
     const int y = y0 + (d >> 1), x = x0 + (d & 1);
-    if (y < 0 || y >= H || x < 0 || x >= W || Y < pb || X < pb || Y >= Ho - pa || X >= Wo - pa) continue;
+    ok[d] = !(y < 0 || y >= H || x < 0 || x >= W || Y < pb || X < pb || Y >= Ho - pa || X >= Wo - pa);
+    const int yy = ok[d] ? y : 0, xx = ok[d] ? x : 0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      float v;
       if constexpr (U8) {
-        v = (float)((const uint8_t*)src)[(((size_t)n * H + y) * W + x) * 3 + c];
+        v[d][c] = (float)((const uint8_t*)src)[(((size_t)n * H + yy) * W + xx) * 3 + c];
       } else {  // planar [clip][3][frames][H][W]: image n = clip * frames + frame
         const int b = n / frames, f = n - b * frames;
-        v = ((const float*)src)[((((size_t)b * 3 + c) * frames + f) * H + y) * W + x];
+        v[d][c] = ((const float*)src)[((((size_t)b * 3 + c) * frames + f) * H + yy) * W + xx];
       }
-      const uint16_t h = T::from_f32((v / div - mean[c]) / sd[c]);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    if (!ok[d]) continue;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const uint16_t h = T::from_f32((v[d][c] / div - mean[c]) / sd[c]);
       if (d < 2) lo[d * 4 + c] = h; else hi[(d - 2) * 4 + c] = h;
     }
   }

@@ -424,6 +424,32 @@ def test_max_pool_3x3x3_s1_lds14(dt, d, c):
     assert torch.equal(bc[..., 8:8 + c], r) and bc[..., :8].abs().max() == 0 and bc[..., 8 + c:].abs().max() == 0
 
 
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("h,w,pb,pa", [(30, 26, 2, 1), (224, 224, 2, 1), (18, 16, 0, 0)])
+def test_pack_input_s2d_u8_cells(h, w, pb, pa, dt):
+    """fac_pack_input_s2d on uint8 NHWC images (ResNet-50's conv1 input,
+    /255 + ImageNet normalisation): every 16-channel cell is the
+    normalised 2x2 pixel block (pixel (dy, dx) in channels 4(2dy+dx) + c,
+    channel 3 of each pixel zero), the border cells zero — bit-equal to the
+    same arithmetic in fp32 rounded once."""
+    from fac_fake_amd.ops import TORCH16, pack_input_s2d
+    g = torch.Generator().manual_seed(h + w)
+    img = torch.randint(0, 256, (3, h, w, 3), generator=g, dtype=torch.uint8)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    out = pack_input_s2d(img.to(DEV), dtype=dt, u8=True, div=255.0, mean=mean, std=std, pad_before=pb,
+                         pad_after=pa)
+    torch.cuda.synchronize()
+    ho, wo = h // 2 + pb + pa, w // 2 + pb + pa
+    ref = torch.zeros(3, 1, ho, wo, 16)
+    x = (img.float() / 255.0 - torch.tensor(mean)) / torch.tensor(std)
+    for dy in range(2):
+        for dx in range(2):
+            blk = x[:, dy:2 * (h // 2):2, dx:2 * (w // 2):2, :]          # [3, h/2, w/2, 3]
+            ref[:, 0, pb:pb + h // 2, pb:pb + w // 2, 4 * (2 * dy + dx):4 * (2 * dy + dx) + 3] = blk
+    assert tuple(out.shape) == (3, 1, ho, wo, 16)
+    assert torch.equal(out.cpu().float(), ref.to(TORCH16[dt]).float())
+
+
 def test_kan_linear_vs_reference(golden):
     from fac_fake_amd.ops import KANLinearLayer
     g = golden("resvitkan_golden.npz")
