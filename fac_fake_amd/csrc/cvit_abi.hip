@@ -764,7 +764,7 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     fac::set_nd_occ3(value);
     return FAC_OK;
   }
-  if (k == "nd_pt_wide") {  // convnd_pt for cout % 128 != 0 from this many 256-row tiles (default 256; 0: off); process-wide
+  if (k == "nd_pt_wide") {  // convnd_pt for cout % 128 != 0 from this many 256-row tiles (default 32; 0: off); process-wide
     if (value < 0) return set_err(c, FAC_ERR_ARG, "nd_pt_wide must be >= 0");
     fac::set_nd_pt_wide(value);
     return FAC_OK;

@@ -2517,7 +2517,7 @@ static dim3 conv_grid(ConvP& p, int gx, int ny) {
 // process-wide (fac_set_option "nd_pt_wide"): convnd_pt also for cout not a
 // multiple of 128 (a partial last column block) from this many 256-row tiles
 // on; 0 keeps those on convnd_igemm (A/B)
-static int g_nd_pt_wide = 256;
+static int g_nd_pt_wide = 32;
 void set_nd_pt_wide(int v) { g_nd_pt_wide = v; }
 // process-wide (fac_set_option "nd_occ3"): convnd_igemm's 3-per-CU 2-slot
 // 128 x 64 tile also for cout <= 64 up to this many K steps (default 4: S3D's

@@ -200,7 +200,7 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * bit-identical outputs).  Process-wide knobs of the fac_ops.h layer kernels
  * (A/B measurements; any context sets them): "nd_pt_wide" (n >= 0: convnd_pt
  * also takes uniform-tap convs whose cout is not a multiple of 128, and
- * fac_conv_nd_split's column segments, from n 256-row tiles on; default 256,
+ * fac_conv_nd_split's column segments, from n 256-row tiles on; default 32,
  * 0 = convnd_igemm), "nd_occ3" (convnd_igemm's 3-per-CU 2-slot 128x64 tile
  * for cout <= 64 up to n K steps; default 4, 0 = K <= 128 only), "pool_roll" (MaxPool3d(3,1,1) on 7-wide maps by
  * maxpool3_roll: 1 = every frame in one thread, the default; k >= 2 = k frames

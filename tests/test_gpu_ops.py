@@ -140,7 +140,7 @@ def test_conv_nd_pt_partial_column_block(n, d, h, w, cin, cout, k, pd, c_off, dt
             torch.cuda.synchronize()
             outs[v] = o.cpu()
     finally:
-        _nd_pt_wide(256, dt)
+        _nd_pt_wide(32, dt)
     y = outs[1]
     assert torch.all(y[..., :c_off] == 7.0) and torch.all(y[..., c_off + cout:] == 7.0)
     ref = F.relu(F.conv3d(x, wt.to(T16[dt]).float(), b, padding=pd)).permute(0, 2, 3, 4, 1)
@@ -683,7 +683,7 @@ def test_s3d_graph_replay_matches_eager(s3d_models):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
-@pytest.mark.parametrize("pt_wide,shape", [(256, (2, 4, 7, 7)), (1, (2, 4, 7, 7)), (1, (3, 8, 14, 14))])
+@pytest.mark.parametrize("pt_wide,shape", [(32, (2, 4, 7, 7)), (1, (2, 4, 7, 7)), (1, (3, 8, 14, 14))])
 def test_conv_split_equals_separate_convs(dt, pt_wide, shape):
     """fac_conv_nd_split over concatenated weights (S3D's merged Inception
     heads) writes exactly what three separate fac_conv_nd launches write:
@@ -696,7 +696,7 @@ def test_conv_split_equals_separate_convs(dt, pt_wide, shape):
     try:
         _split_case(g, n, d, h, w, cin, widths, dt)
     finally:
-        _nd_pt_wide(256, dt)
+        _nd_pt_wide(32, dt)
 
 
 def _split_case(g, n, d, h, w, cin, widths, dt):
