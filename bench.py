@@ -471,9 +471,78 @@ def repbn8_measurement(dev, dtype: str, world: int, B: int = 256, steps: int = 1
             "mfma_roofline_fraction": round(v * REPBN8_FLOP_PER_CROP / (world * PEAK_TFLOPS[dtype] * 1e12), 4)}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N
+    fresh copies of this script, one per GPU (RANK = LOCAL_RANK = i,
+    WORLD_SIZE = N, rendezvous on 127.0.0.1), the way the reference's DDP
+    script spawns its `world_size` local workers
+    (sx_exp_deepfakedetect-master/S3D/S3D-train-GPUs.py:580-585).  This
+    parent never touches the GPU (no HIP call, no torch.cuda init: counting
+    devices does not initialise it), so the children are plain child
+    processes, not an exec of a GPU-initialised one.  Rank 0's stdout carries
+    the JSON line.  If a rank fails the others are terminated; returns the
+    first non-zero exit code (0 when every rank succeeded)."""
+    import subprocess
+    gloo = os.environ.get("FAC_DIST_BACKEND", "nccl") != "nccl"
+    if not gloo:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"[bench] --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FAC_BENCH_LAUNCHER="bench.py --gpus (spawn)")
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:   # a dead rank would leave the others waiting in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc if rc >= 0 else 1
+
+
+def launch_info(backend: str, world: int, rank: int, local: int) -> dict:
+    """Which ranks the process group saw (every rank reports its rank, local
+    rank, device and host pid through one all_gather_object)."""
+    me = {"rank": rank, "local_rank": local, "pid": os.getpid(),
+          "device": (torch.cuda.get_device_name(local) if backend == "nccl" else "cpu")}
+    seen = [me]
+    if world > 1:
+        seen = [None] * world
+        dist.all_gather_object(seen, me)
+    return {"launcher": os.environ.get("FAC_BENCH_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                       else ("external" if world > 1 else "single process")),
+            "backend": backend if world > 1 else None, "world_size": world,
+            "ranks_seen": [s["rank"] for s in seen], "local_ranks": [s["local_rank"] for s in seen],
+            "devices": [s["device"] for s in seen]}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without torchrun's WORLD_SIZE the script spawns them itself")
+    ap.add_argument("--dist-check", action="store_true",
+                    help="launch + rendezvous + rank all-gather only, no measurement (the N>1 launcher's CPU test "
+                         "with FAC_DIST_BACKEND=gloo)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
@@ -501,20 +570,36 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks here, before anything touches the GPU
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("FAC_DIST_BACKEND", "nccl") != "nccl":
+    if world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
+    # RCCL over xGMI; FAC_DIST_BACKEND=gloo only to rehearse the multi-rank
+    # control flow with several ranks on one GPU (RCCL refuses that) or, with
+    # --dist-check, on a host without a GPU
+    backend = os.environ.get("FAC_DIST_BACKEND", "nccl")
+    if backend != "nccl" and not args.dist_check:
         local %= max(torch.cuda.device_count(), 1)   # rehearsal: several ranks may share a GPU
     if world > 1:
-        torch.cuda.set_device(local)
-        # RCCL over xGMI; FAC_DIST_BACKEND=gloo only to rehearse the multi-rank
-        # control flow with several ranks on one GPU (RCCL refuses that)
-        backend = os.environ.get("FAC_DIST_BACKEND", "nccl")
         if backend == "nccl":
+            torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
+            if not args.dist_check:
+                torch.cuda.set_device(local)
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    launch = launch_info(backend, world, rank, local)
+    if args.dist_check:
+        if rank == 0:
+            print(json.dumps({"dist_check": True, "n_gpus": world, "launch": launch}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     dev = torch.device("cuda", local)
     B = args.batch
     if args.only and args.opt:
@@ -570,6 +655,7 @@ def main():
                    "fused_stem224": not args.no_fuse, "pipelined": r["pipelined"],
                    **({"options": args.opt} if args.opt else {})},
         "mfma_roofline_fraction": round(value * FLOP_PER_CROP / (world * peak * 1e12), 4),
+        "launch": launch,
         "parity": r["parity"],
         "roofline": r["roofline"],
         "stage_ms": r["stage_ms"],

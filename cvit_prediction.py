@@ -132,9 +132,24 @@ def predict_on_video(dfdc_filenames, num_workers, batch: int = 256):
         frames, boxes = read_video(os.path.join(sample, dfdc_filenames[i]))
         return select_reference(frames, boxes)
 
+    # read-ahead is bounded: at most num_workers + 1 loaded videos wait for
+    # the GPU (each holds its selected host frames, ~190 MB at 1080p; the
+    # reference's threads only ever hold float scores)
+    from collections import deque
+    workers = max(1, int(num_workers))
+    n = len(dfdc_filenames)
+
+    def items(ex):
+        pending, nxt = deque(), 0
+        while nxt < n or pending:
+            while nxt < n and len(pending) < workers + 1:
+                pending.append(ex.submit(load, nxt))
+                nxt += 1
+            yield pending.popleft().result()
+
     predictions, group, ncrops = [], [], 0
-    with ThreadPoolExecutor(max_workers=max(1, int(num_workers))) as ex:
-        for item in ex.map(load, range(len(dfdc_filenames))):
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        for item in items(ex):
             if group and ncrops + len(item[1]) > batch:
                 predictions += score_selected(model, group, batch)
                 group, ncrops = [], 0

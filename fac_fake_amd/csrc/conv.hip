@@ -597,266 +597,6 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restric
   store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
 }
 
-// ---------------------------------------------------------------------------
-// conv45_fused: CViT conv4 -> conv5 (cvit.py:99-107: 112^2, 32 -> 64 -> 64,
-// folded BN + ReLU each) in one launch.  A workgroup owns one 16 x 16 box of
-// conv5's output and computes conv4 on the 18 x 18 region conv5 reads
-// (1.27x conv4's MACs), so conv4's 411 MB output never goes through HBM and
-// its per-box prologue / epilogue happen once for both layers.
-//
-//   IN (20 x 20 input pixels x 32 ch, pixel-major, row pitch 21: the
-//   window-major 18 x 18 tiles' fragment reads then average 1.05-way over
-//   every tap, simulated over the ds_read_b128 lane groups)
-//     -> conv4, transposed MFMAs (rows = channels), 24 row tiles of 16
-//        pixels (324 used) over 4 waves, 9 taps
-//     -> bias + ReLU (zero outside the image = conv5's padding) -> C4
-//        (18 x 18 x 64 as two pixel-major 32-channel planes, the halo image
-//        conv3x3_bn_relu would have loaded; ALIASES IN, dead by then)
-//     -> conv5, conv3x3_bn_relu's 16 x 16 tile (window-major, 4 x 1 waves),
-//        2 chunks x 9 taps, both chunks resident (no halo reload)
-//     -> bias + ReLU -> LDS staging (aliases C4) -> 16-byte stores.
-// The 27 weight slices (9 of conv4, 18 of conv5) stream through one 3-slot
-// LDS ring, slice s issued at step s-3 and its fragments read into
-// registers during step s-1 (conv3x3_bn_relu's PB schedule).
-// conv4's outputs are rounded to 16 bits before conv5 exactly as the
-// unfused path stores them, and both convs keep their k order: the output is
-// bit-identical to conv4 then conv5 (test_conv45_fused_equals_unfused).
-// Measured (round 4, same box, three alternations): 0.417 ms against
-// 0.401 ms for the two launches, CViT within noise (85.3k vs 85.1k) -- the
-// 1.17x MFMAs (conv4 on 384 rows for 324 pixels, the 18x18 halo) eat what
-// the dropped HBM round trip and prologue save, and at 214 VGPRs only two
-// workgroups share a CU.  Off by default (fac_set_option "fuse45").
-template <class T>
-__global__ __launch_bounds__(256, 2) void conv45_fused(const uint16_t* __restrict__ in,
-                                                       const uint16_t* __restrict__ w4,
-                                                       const float* __restrict__ b4,
-                                                       const uint16_t* __restrict__ w5,
-                                                       const float* __restrict__ b5, uint16_t* __restrict__ out,
-                                                       const uint16_t* __restrict__ zero16) {
-  constexpr int H = 112, W = 112, TH = 16, TW = 16, BN = 64, CK = CONV_CK;
-  constexpr int G4 = TH + 2;                       // conv4's output region (conv5's halo): 18 x 18
-  constexpr int NP4 = G4 * G4;                     // 324 pixels
-  constexpr int IN_H = G4 + 2, IN_RPX = IN_H + 1;  // conv4's input region 20 x 20, row pitch 21
-  constexpr int IN_SLOTS = (IN_H * IN_RPX * 4 + 255) / 256 * 256;
-  constexpr int HPW = IN_SLOTS / 256;
-  constexpr int C4_RPX = G4, C4_PLANE = G4 * C4_RPX * 4 * 8;  // elements per 32-channel plane
-  constexpr int WSL = BN * CK;
-  constexpr int RTW4 = 6, RTW5 = 4, CTW = 4;  // row tiles per wave (conv4: 24 x 16 rows >= 324), channel tiles
-  constexpr int OPS = BN + 8;
-  constexpr int REGION_A = IN_SLOTS * 8, REGION_B = 2 * C4_PLANE, REGION_C = TH * TW * OPS;
-  constexpr int REGION = REGION_A > REGION_B ? (REGION_A > REGION_C ? REGION_A : REGION_C)
-                                             : (REGION_B > REGION_C ? REGION_B : REGION_C);
-  static_assert(RTW4 * 4 * 16 >= NP4, "conv4 rows");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[REGION + 3 * WSL];
-  uint16_t* const img = smem;  // IN, then C4, then the output staging tile
-  uint16_t* const ring = smem + REGION;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  int bx = blockIdx.x;  // XCD-aware box order (conv3x3_bn_relu)
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  constexpr int TILES_X = W / TW, TILES = (H / TH) * TILES_X;
-  const int b = bx / TILES;
-  const int tile = bx - b * TILES;
-  const int ty = tile / TILES_X, tx = tile - ty * TILES_X;
-  const int y0 = ty * TH, x0 = tx * TW;
-
-  // slice s of the 27: conv4's 9 taps, then conv5's 2 chunks x 9 taps
-  auto issue_w = [&](int slot, int s) {
-    const uint16_t* src = s < 9 ? w4 + (size_t)s * WSL : (s < 27 ? w5 + (size_t)(s - 9) * WSL : w4);  // past 26: dummy
-    glds16(src + (size_t)(wave * 64 + lane) * 8, ring + slot * WSL + wave * 64 * 8);
-  };
-  issue_w(0, 0);
-  issue_w(1, 1);
-  issue_w(2, 2);
-  // IN: slot (i*4 + wave)*64 + lane of the pixel-major image holds 16 bytes
-  // of pixel (hy, hx) (input pixel (y0-2+hy, x0-2+hx)), channel piece q
-#pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    const int slot = (i * 4 + wave) * 64 + lane;
-    const int pix = slot >> 2;
-    const int hy = pix / IN_RPX, hx = pix - (pix / IN_RPX) * IN_RPX;
-    const int q = hy < IN_H ? (slot & 3) ^ ((hy & 1) << 1) : 4;
-    const int y = y0 - 2 + hy, x = x0 - 2 + hx;
-    const bool ok = q < 4 && hx < IN_H && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-    glds16(ok ? in + (((size_t)b * H + y) * W + x) * CK + q * 8 : zero16, img + (i * 4 + wave) * 64 * 8);
-  }
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-
-  // weight (A operand of conv4's transposed MFMAs, B of conv5's) fragment of channel tile ct
-  int bbase[CTW];
-#pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) bbase[ct] = (g * BN + ct * 16 + (lane & 15)) * 8;
-  // B fragments one step ahead (conv3x3_bn_relu's PB): step s multiplies
-  // slice s from registers (read during step s-1), reads slice s+1 behind
-  // its first row tile's MFMAs, and refills slot s % 3 with slice s+3
-  u16x8 bcur[CTW];
-#pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) bcur[ct] = *(const u16x8*)(ring + bbase[ct]);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // slot 0 is refilled at step 0
-
-  // ---- conv4 over the 18 x 18 region (window-major pixel order)
-  int abase4[RTW4];
-#pragma unroll
-  for (int rt = 0; rt < RTW4; ++rt) {
-    int m = (wave * RTW4 + rt) * 16 + (lane & 15);
-    if (m >= NP4) m = 0;  // padding rows: computed on pixel 0, never written
-    int py, px;
-    box_pixel<G4>(m, py, px);
-    abase4[rt] = ((py * IN_RPX + px) * 4 + (g ^ ((py & 1) << 1))) * 8;
-  }
-  f32x4 acc4[RTW4][CTW];
-#pragma unroll
-  for (int rt = 0; rt < RTW4; ++rt)
-#pragma unroll
-    for (int ct = 0; ct < CTW; ++ct) acc4[rt][ct] = (f32x4)0.f;
-  u16x8 fa4[RTW4];
-#pragma unroll
-  for (int rt = 0; rt < RTW4; ++rt) fa4[rt] = *(const u16x8*)(img + abase4[rt]);
-
-  auto step4 = [&](auto tc) {
-    constexpr int t = decltype(tc)::value;
-    issue_w(t % 3, t + 3);
-    const uint16_t* wbn = ring + ((t + 1) % 3) * WSL;
-    u16x8 bfr[CTW], bnx[CTW];
-#pragma unroll
-    for (int ct = 0; ct < CTW; ++ct) bfr[ct] = bcur[ct];
-    constexpr int kyn = (t + 1) / 3, kxn = (t + 1) % 3;
-    constexpr int ntoff = (kyn * IN_RPX + kxn) * 32;
-#pragma unroll
-    for (int rt = 0; rt < RTW4; ++rt) {
-#pragma unroll
-      for (int ct = 0; ct < CTW; ++ct) acc4[rt][ct] = T::mfma(bfr[ct], fa4[rt], acc4[rt][ct]);
-      if (rt == 0) {
-#pragma unroll
-        for (int ct = 0; ct < CTW; ++ct) bnx[ct] = *(const u16x8*)(wbn + bbase[ct]);
-      }
-      if constexpr (t < 8) fa4[rt] = *(const u16x8*)(img + abase4[rt] + ntoff);
-    }
-#pragma unroll
-    for (int ct = 0; ct < CTW; ++ct) bcur[ct] = bnx[ct];
-    __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, CTW + (t < 8 ? 1 : 0), 0);
-#pragma unroll
-    for (int rt = 1; rt < RTW4; ++rt) {
-      __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
-      if constexpr (t < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    // slice t+2 landed (t+3 stays in flight); every wave is past its reads
-    // of slot (t+1) % 3, which step t+1 refills
-    asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  step4(std::integral_constant<int, 0>{});
-  step4(std::integral_constant<int, 1>{});
-  step4(std::integral_constant<int, 2>{});
-  step4(std::integral_constant<int, 3>{});
-  step4(std::integral_constant<int, 4>{});
-  step4(std::integral_constant<int, 5>{});
-  step4(std::integral_constant<int, 6>{});
-  step4(std::integral_constant<int, 7>{});
-  step4(std::integral_constant<int, 8>{});
-
-  // conv4 epilogue -> C4 (IN is dead: every wave passed step 8's barrier).
-  // A lane holds channels ct*16 + 4g .. +3 of pixel m: 8 bytes of piece
-  // (ct & 1)*2 + (g >> 1) of plane ct >> 1, at its row-parity position.
-#pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) {
-    const f32x4 bb = *(const f32x4*)(b4 + ct * 16 + 4 * g);
-#pragma unroll
-    for (int rt = 0; rt < RTW4; ++rt) {
-      const int m = (wave * RTW4 + rt) * 16 + (lane & 15);
-      if (m < NP4) {
-        int py, px;
-        box_pixel<G4>(m, py, px);
-        const bool inside = (unsigned)(y0 - 1 + py) < (unsigned)H && (unsigned)(x0 - 1 + px) < (unsigned)W;
-        f32x4 v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = inside ? relu(acc4[rt][ct][j] + bb[j]) : 0.f;
-        const int piece = (ct & 1) * 2 + (g >> 1);
-        const int pos = piece ^ ((py & 1) << 1);
-        *(u16x4*)(img + (ct >> 1) * C4_PLANE + ((py * C4_RPX + px) * 4 + pos) * 8 + (g & 1) * 4) = T::pack4(v);
-      }
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-
-  // ---- conv5 over the 16 x 16 box from C4 (conv3x3_bn_relu's 112^2 tile)
-  int abase5[RTW5];
-#pragma unroll
-  for (int rt = 0; rt < RTW5; ++rt) {
-    int py, px;
-    box_pixel<TW>((wave * RTW5 + rt) * 16 + (lane & 15), py, px);
-    abase5[rt] = ((py * C4_RPX + px) * 4 + (g ^ ((py & 1) << 1))) * 8;
-  }
-  f32x4 acc[RTW5][CTW];
-#pragma unroll
-  for (int rt = 0; rt < RTW5; ++rt)
-#pragma unroll
-    for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = (f32x4)0.f;
-  u16x8 fa[RTW5];
-#pragma unroll
-  for (int rt = 0; rt < RTW5; ++rt) fa[rt] = *(const u16x8*)(img + abase5[rt]);
-
-  auto step5 = [&](auto cc, auto tc) {
-    constexpr int c = decltype(cc)::value, t = decltype(tc)::value, s = 9 + 9 * c + t;
-    issue_w(s % 3, s + 3);  // past slice 26: a dummy re-read into a dead slot
-    const uint16_t* wbn = ring + ((s + 1) % 3) * WSL;
-    u16x8 bfr[CTW], bnx[CTW];
-#pragma unroll
-    for (int ct = 0; ct < CTW; ++ct) bfr[ct] = bcur[ct];
-    constexpr bool more = t < 8 || c == 0;
-    constexpr int kyn = t < 8 ? (t + 1) / 3 : 0, kxn = t < 8 ? (t + 1) % 3 : 0;
-    constexpr int ntoff = (t < 8 ? c : 1) * C4_PLANE + (kyn * C4_RPX + kxn) * 32;
-#pragma unroll
-    for (int rt = 0; rt < RTW5; ++rt) {
-#pragma unroll
-      for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
-      if (rt == 0) {
-#pragma unroll
-        for (int ct = 0; ct < CTW; ++ct) bnx[ct] = *(const u16x8*)(wbn + bbase[ct]);
-      }
-      if constexpr (more) fa[rt] = *(const u16x8*)(img + abase5[rt] + ntoff);
-    }
-#pragma unroll
-    for (int ct = 0; ct < CTW; ++ct) bcur[ct] = bnx[ct];
-    __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, CTW + (more ? 1 : 0), 0);
-#pragma unroll
-    for (int rt = 1; rt < RTW5; ++rt) {
-      __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
-      if constexpr (more) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  step5(I0{}, std::integral_constant<int, 0>{});
-  step5(I0{}, std::integral_constant<int, 1>{});
-  step5(I0{}, std::integral_constant<int, 2>{});
-  step5(I0{}, std::integral_constant<int, 3>{});
-  step5(I0{}, std::integral_constant<int, 4>{});
-  step5(I0{}, std::integral_constant<int, 5>{});
-  step5(I0{}, std::integral_constant<int, 6>{});
-  step5(I0{}, std::integral_constant<int, 7>{});
-  step5(I0{}, std::integral_constant<int, 8>{});
-  step5(I1{}, std::integral_constant<int, 0>{});
-  step5(I1{}, std::integral_constant<int, 1>{});
-  step5(I1{}, std::integral_constant<int, 2>{});
-  step5(I1{}, std::integral_constant<int, 3>{});
-  step5(I1{}, std::integral_constant<int, 4>{});
-  step5(I1{}, std::integral_constant<int, 5>{});
-  step5(I1{}, std::integral_constant<int, 6>{});
-  step5(I1{}, std::integral_constant<int, 7>{});
-  step5(I1{}, std::integral_constant<int, 8>{});
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy slices landed before LDS is reused / the wave ends
-
-  // conv5 epilogue (C4 is dead: every wave passed the last step's barrier)
-  stage_tile<T, RTW5, CTW, OPS, false, true>(acc, img, b5, wave, 0, lane);
-  __syncthreads();
-  store_tile<TH, TW, BN, false>(img, out, b, H, W, y0, x0, BN, 0, tid);
-}
-
 // conv1 (3 -> 32 @224) with the input normalisation of cvit_prediction.py:
 // x/255 then (x - mean_c)/std_c (:41-42, :214-215), zero padding applied in
 // normalised space exactly like the reference's Conv2d(padding=1).
@@ -1031,30 +771,20 @@ static hipError_t launch_db(const uint16_t* in, const uint16_t* wpk, const float
 }
 
 
-// conv3x3_db for the 28^2 tiles (fac_set_option "conv_db": 1 = on, the
-// default; 0 = conv3x3_bn_relu, for A/Bs).  Same box, bit-identical outputs
-// (tools/db_ab.py, round 4): conv10-13 101.7/178.2/177.2/163.2 ->
-// 91.1/164.8/165.6/153.4 us.  At 56^2 it was neutral (B shared by two waves
-// of the 2x2 grid doubles its L2 reads), at 14^2 slower (the 1x4 tile needs
-// ~280 VGPRs and spills; the 2x2 tile pads 196 pixels to 224 rows), at
-// 112^2 15-20 % slower (four waves re-read the same B): those keep the LDS
-// weight ring.
-static int g_conv_db = 1;
-void set_conv_db(int v) { g_conv_db = v; }
+// conv3x3_db for the 28^2 tiles.  Same box, bit-identical outputs
+// (tools/archive/db_ab.py, round 4): conv10-13 101.7/178.2/177.2/163.2 ->
+// 91.1/164.8/165.6/153.4 us against the LDS weight ring (that arm, option
+// "conv_db" 0, was removed in round 5).  At 56^2 it was neutral (B shared by
+// two waves of the 2x2 grid doubles its L2 reads), at 14^2 slower (the 1x4
+// tile needs ~280 VGPRs and spills; the 2x2 tile pads 196 pixels to 224
+// rows), at 112^2 15-20 % slower (four waves re-read the same B): those keep
+// the LDS weight ring.
 
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                                 int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st,
                                 int relu) {
   if (W != H) return hipErrorInvalidValue;
-  if (g_conv_db) {
-    switch (H * 1000 + conv_block_n(H, Cout)) {
-      case 28256: return launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      case 28192: return launch_db<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      case 28128: return launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      default: break;
-    }
-  }
   switch (H * 1000 + conv_block_n(H, Cout)) {
     case 224032: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
@@ -1069,9 +799,9 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
       break;
     case 56128: launch_box<T, 8, 28, 128, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 56064: launch_box<T, 8, 28, 64, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 28256: launch_box<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 28192: launch_box<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 28128: launch_box<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28256: launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28192: launch_db<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28128: launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // (a two-box 14x14 workgroup needs 256+ VGPRs and spills: not built)
     case 14128: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 14192:
@@ -1089,16 +819,6 @@ hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, co
                           bool relu) {
   if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu);
   return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu);
-}
-
-// CViT conv4 -> conv5 fused (conv45_fused): in [B,112,112,32] -> out
-// [B,112,112,64]; w4 / w5 packed by pack_conv3x3 for H = 112.
-hipError_t launch_conv45(int dtype, const uint16_t* in, const uint16_t* w4, const float* b4, const uint16_t* w5,
-                         const float* b5, uint16_t* out, int B, const uint16_t* zero16, hipStream_t st) {
-  const dim3 grid(B * 49);
-  if (dtype == 0) conv45_fused<BF16><<<grid, 256, 0, st>>>(in, w4, b4, w5, b5, out, zero16);
-  else conv45_fused<F16><<<grid, 256, 0, st>>>(in, w4, b4, w5, b5, out, zero16);
-  return hipGetLastError();
 }
 
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,

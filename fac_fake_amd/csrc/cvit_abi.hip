@@ -22,7 +22,6 @@
 
 namespace fac {
 int conv_block_n(int H, int cout);
-void set_conv_db(int v);
 void set_nd_pt_wide(int v);
 void set_nd_occ3(int v);
 void set_pool_roll(int v);
@@ -33,8 +32,6 @@ void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* ou
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, bool relu = true);
-hipError_t launch_conv45(int dtype, const uint16_t* in, const uint16_t* w4, const float* b4, const uint16_t* w5,
-                         const float* b5, uint16_t* out, int B, const uint16_t* zero16, hipStream_t st);
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
                         int B, int H, int W, hipStream_t st);
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
@@ -58,7 +55,7 @@ hipError_t launch_crop_resize(const uint8_t* frames, int n_frames, int H, int W,
                               uint8_t* crops, hipStream_t st);
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
-                          hipStream_t s, int* sched = nullptr);
+                          hipStream_t s);
 enum { EPI_F32 = 0, EPI_F32_RELU = 1, EPI_T_GELU = 2, EPI_RESID = 3, EPI_PARTIAL = 4, EPI_T = 5 };
 }  // namespace fac
 
@@ -121,7 +118,6 @@ struct fac_ctx {
   int cap_B = 0;
   int stem_chunk = 0;
   int fuse_stem224 = 1;  // conv1..conv3+pool as one persistent kernel (stem224.hip)
-  int fuse45 = 0;        // 1: conv4 -> conv5 as one kernel (conv.hip conv45_fused; measured neutral, off)
   // GEMM tile variant per call site (transformer.hip launch_gemm; -1 = default)
   // and the split-K factor of the two N=1024 projections (to_out, FF2)
   int gemm_var[6] = {-1, -1, -1, -1, -1, -1};  // patch, qkv, out, ff1, ff2, head
@@ -147,9 +143,12 @@ struct fac_ctx {
   // host at the start of the next forward without a device sync
   int* errflag = nullptr;      // device view
   int* err_host = nullptr;     // host view of the same int
-  int fwd_seq = 0;             // forwards on this context (the flag holds the offending one's number)
-  int* sched = nullptr;  // 2 ints: stem224 dynamic box counter + finished-workgroup count
-  int stem_dynamic = 0;  // option "stem_dynamic": stem224 claims boxes from `sched` (default: static, no atomics)
+  // encoder launches on this context (the flag holds the offending one's
+  // number).  It counts tail launches, not API calls: a pipelined or chunked
+  // call counts once per batch, and a captured graph (the small-batch replay
+  // or a caller's capture) bakes in the number of its capture, which every
+  // replay then reports.
+  int fwd_seq = 0;
   int stem_nwg = 0;      // option "stem_nwg": persistent stem workgroups (0 = one per CU)
   // option "stem_events": hipEvent pairs around every fused-stem launch (the
   // bench's timed region), read back by fac_stem_event_ms
@@ -157,14 +156,35 @@ struct fac_ctx {
   std::vector<hipEvent_t> stem_evs;
   size_t stem_ev_used = 0;
   uint16_t* zero16 = nullptr;  // 256 zero bytes: the source of zero-padding glds pieces
-  // Conv stacks of one context share the activation buffers and the stem's
-  // box counter (`sched`), so two of them must never overlap: every conv
-  // stack records ev_stack on its stream, and a conv stack enqueued on a
-  // different stream first waits for it.  (Inside a stream capture the
-  // caller orders the graph launches; no external event is waited on there.)
+  // Forwards of one context share the activation and encoder buffers, so two
+  // of them must never overlap on the device: every forward records ev_stack
+  // on its stream after its last kernel (a synchronous forward: after the
+  // head; a pipelined one: after its conv stack, its tail being ordered by
+  // ev_tail), and a forward enqueued on a different stream first waits for
+  // it.  Threads that share a context therefore need no common stream.
+  // (Inside a stream capture the caller orders the graph launches; no
+  // external event is waited on there.)
   hipEvent_t ev_stack = nullptr;
   hipStream_t stack_st = nullptr;
   bool stack_rec = false;
+  // Small-batch graph replay (option "graph_max_b"): a forward of B <= this
+  // many crops on a stream that is not being captured replays a hipGraph of
+  // the whole forward, captured once per (B, input kind, probs) on cap_st
+  // over context-owned input / slot / output buffers (g_in_*, g_pidx,
+  // g_out).  The reference scores a video as ONE <= 29-crop call
+  // (cvit_prediction.py:224-229), whose ~60 kernels are latency-bound at
+  // that size: the graph turns them into one launch.
+  struct SmallGraph {
+    int B, kind;  // kind: bit 0 = uint8 NHWC input, bit 1 = probs wanted
+    hipGraphExec_t exec;
+  };
+  int graph_max_b = 32;
+  std::vector<SmallGraph> graphs;
+  hipStream_t cap_st = nullptr;
+  void* g_in[2] = {nullptr, nullptr};  // [0] fp32 NCHW, [1] uint8 NHWC; graph_max_b crops each
+  int32_t* g_pidx = nullptr;
+  float* g_out = nullptr;  // logits [graph_max_b][2], then probs [graph_max_b][2]
+  int g_cap = 0;           // crops the g_* buffers hold
 };
 
 namespace {
@@ -181,10 +201,10 @@ int take_device_error(fac_ctx* c) {
   if (c && c->err_host && *(volatile int*)c->err_host) {
     const int bad = *(volatile int*)c->err_host;
     *(volatile int*)c->err_host = 0;
-    return set_err(c, FAC_ERR_ARG, "forward call #" + std::to_string(bad) + " of this context (this call is #" +
+    return set_err(c, FAC_ERR_ARG, "encoder launch #" + std::to_string(bad) + " of this context (the next is #" +
                                        std::to_string(c->fwd_seq + 1) +
-                                       ") had a pos_index outside [0,32), clamped on the device; this call was "
-                                       "not run");
+                                       "; graph replays report their capture's number) had a pos_index outside "
+                                       "[0,32), clamped on the device; this call was not run");
   }
   return 0;
 }
@@ -210,7 +230,7 @@ hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, ui
 }
 
 struct WsLayout {
-  size_t act, deep, stem, stem2, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, sched, zero, total;
+  size_t act, deep, stem, stem2, slab, x, xn, qkv, o, hbuf, cbuf, hh, err, zero, total;
   int cb;  // crops the high-res activation buffers hold (stem chunk)
 };
 
@@ -241,14 +261,24 @@ WsLayout layout(int B, int chunk) {
   L.cbuf = off; off += al((size_t)B * kDim * 2);
   L.hh = off; off += al((size_t)B * kMlp * 4);
   L.err = off; off += 256;
-  L.sched = off; off += 256;
   L.zero = off; off += 256;
   L.total = off;
   return L;
 }
 
+// Drop the captured small-batch graphs (they hold the workspace and weight
+// pointers and the kernel choices of the options they were captured with):
+// on a workspace reallocation, a weight load, an option change or destroy.
+void drop_graphs(fac_ctx* c) {
+  if (c->graphs.empty()) return;
+  (void)hipDeviceSynchronize();  // no replay of them is still in flight
+  for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
+  c->graphs.clear();
+}
+
 int ensure_ws(fac_ctx* c, int B) {
   if (B <= c->cap_B && c->ws) return FAC_OK;
+  drop_graphs(c);
   const WsLayout L = layout(B, c->stem_chunk);
   if (c->ws) {
     HIP_TRY(c, hipDeviceSynchronize());
@@ -287,7 +317,6 @@ int ensure_ws(fac_ctx* c, int B) {
     HIP_TRY(c, hipHostGetDevicePointer(&dp, hp, 0));
     c->errflag = (int*)dp;
   }
-  c->sched = (int*)(base + L.sched);  // stem224 box counters (zeroed above, self-resetting)
   c->zero16 = (uint16_t*)(base + L.zero);  // the whole workspace was just zeroed
   c->ws_bytes = L.total;
   c->cap_B = B;
@@ -552,8 +581,7 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
         HIP_TRY(c, hipEventRecord(sev0, st));
       }
       HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_wp, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
-                                c->conv[1].b, cur, nb, c->stem_nwg > 0 ? c->stem_nwg : c->num_cu, st,
-                                c->stem_dynamic ? c->sched : nullptr));
+                                c->conv[1].b, cur, nb, c->stem_nwg > 0 ? c->stem_nwg : c->num_cu, st));
       if (sev1) HIP_TRY(c, hipEventRecord(sev1, st));
       MARK(0);
       l0 = 2;
@@ -572,21 +600,6 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
       }
     }
     for (int l = l0; l <= kLastChunked && !copied; ++l) {
-      if (l == 2 && c->fuse45 && stop_after != 3) {
-        // conv4 -> conv5 in one launch (conv4's output stays in LDS)
-        HIP_TRY(c, launch_conv45(dt, cur, c->conv[2].w, c->conv[2].b, c->conv[3].w, c->conv[3].b, nxt, nb, c->zero16,
-                                 st));
-        MARK(3);
-        MARK(4);
-        if (stop_after == 4) {
-          HIP_TRY(c, hipMemcpyAsync(feat_out + (size_t)b0 * conv_out_elems(c->conv[3]), nxt,
-                                    (size_t)nb * conv_out_elems(c->conv[3]) * 2, hipMemcpyDeviceToDevice, st));
-          copied = true;
-        }
-        std::swap(cur, nxt);
-        ++l;
-        continue;
-      }
       const ConvLayer& L = c->conv[l];
       uint16_t* dst = (l == kLastChunked) ? c->deep0 + (size_t)b0 * conv_out_elems(L) : nxt;
       HIP_TRY(c, run_conv(c, L, cur, dst, nb, st));
@@ -680,6 +693,106 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
   return FAC_OK;
 }
 
+// Order work enqueued on `st` after the context's previous forward on another
+// stream and after any pipelined tail still in flight (fac_ctx::ev_stack).
+int order_on(fac_ctx* c, hipStream_t st) {
+  if (!c->ev_stack) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_stack, hipEventDisableTiming));
+  if (c->stack_rec && c->stack_st != st) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_stack, 0));
+  for (int i = 0; i < 2; ++i)
+    if (c->tail_pending[i]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[i], 0));
+  return FAC_OK;
+}
+
+int mark_done(fac_ctx* c, hipStream_t st) {
+  HIP_TRY(c, hipEventRecord(c->ev_stack, st));
+  c->stack_st = st;
+  c->stack_rec = true;
+  return FAC_OK;
+}
+
+// The small-batch forward by graph replay (fac_ctx::graphs): copy the crops
+// and slots into the context's buffers, launch the graph captured for this
+// (B, kind), copy the logits (and probabilities) out.  The graph holds the
+// same kernels with the same arguments as forward_impl at this B, so the
+// outputs are bit-identical to the eager forward.
+int forward_graph(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
+                  hipStream_t st) {
+  if (int e = take_device_error(c)) return e;
+  DevGuard g(c->device);
+  int rc = ensure_ws(c, B);
+  if (rc) return rc;
+  const size_t crop_bytes = u8 ? (size_t)kImg * kImg * 3 : (size_t)3 * kImg * kImg * 4;
+  if (c->g_cap < c->graph_max_b) {
+    drop_graphs(c);
+    for (void*& p : c->g_in) {
+      if (p) HIP_TRY(c, hipFree(p));
+      p = nullptr;
+    }
+    if (c->g_pidx) HIP_TRY(c, hipFree(c->g_pidx));
+    if (c->g_out) HIP_TRY(c, hipFree(c->g_out));
+    c->g_pidx = nullptr;
+    c->g_out = nullptr;
+    c->g_cap = 0;
+    if (hipMalloc(&c->g_pidx, (size_t)c->graph_max_b * 4) != hipSuccess ||
+        hipMalloc(&c->g_out, (size_t)c->graph_max_b * 16) != hipSuccess)
+      return set_err(c, FAC_ERR_OOM, "graph buffer allocation failed");
+    HIP_TRY(c, hipMemset(c->g_pidx, 0, (size_t)c->graph_max_b * 4));
+    c->g_cap = c->graph_max_b;
+  }
+  void*& gin = c->g_in[u8 ? 1 : 0];
+  if (!gin && hipMalloc(&gin, (size_t)c->g_cap * crop_bytes) != hipSuccess) {
+    gin = nullptr;
+    return set_err(c, FAC_ERR_OOM, "graph input buffer allocation failed");
+  }
+  float* const g_probs = c->g_out + 2 * c->g_cap;
+  const int kind = (u8 ? 1 : 0) | (probs ? 2 : 0);
+  hipGraphExec_t ex = nullptr;
+  for (auto& gr : c->graphs)
+    if (gr.B == B && gr.kind == kind) ex = gr.exec;
+  if (!ex) {
+    if (!c->cap_st) HIP_TRY(c, hipStreamCreateWithFlags(&c->cap_st, hipStreamNonBlocking));
+    // the captured forward must not wait on events recorded outside the
+    // capture; the replay's ordering is done on the caller's stream below
+    const bool tp0 = c->tail_pending[0], tp1 = c->tail_pending[1];
+    c->tail_pending[0] = c->tail_pending[1] = false;
+    HIP_TRY(c, hipStreamBeginCapture(c->cap_st, hipStreamCaptureModeThreadLocal));
+    rc = forward_impl(c, gin, u8, B, c->g_pidx, c->g_out, probs ? g_probs : nullptr, c->cap_st);
+    hipGraph_t graph = nullptr;
+    const hipError_t ec = hipStreamEndCapture(c->cap_st, &graph);
+    c->tail_pending[0] = tp0;
+    c->tail_pending[1] = tp1;
+    if (rc != FAC_OK || ec != hipSuccess) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc != FAC_OK ? rc : set_err(c, FAC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(ec));
+    }
+    const hipError_t ei = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) return set_err(c, FAC_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
+    c->graphs.push_back({B, kind, ex});
+  }
+  rc = order_on(c, st);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(gin, in, (size_t)B * crop_bytes, hipMemcpyDeviceToDevice, st));
+  HIP_TRY(c, hipMemcpyAsync(c->g_pidx, pidx, (size_t)B * 4, hipMemcpyDeviceToDevice, st));
+  HIP_TRY(c, hipGraphLaunch(ex, st));
+  HIP_TRY(c, hipMemcpyAsync(logits, c->g_out, (size_t)B * 8, hipMemcpyDeviceToDevice, st));
+  if (probs) HIP_TRY(c, hipMemcpyAsync(probs, g_probs, (size_t)B * 8, hipMemcpyDeviceToDevice, st));
+  return mark_done(c, st);
+}
+
+// fac_forward_nchw_f32 / fac_forward_nhwc_u8: small batches on a stream that
+// is not being captured replay a graph, everything else runs eagerly.
+int forward_entry(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
+                  void* stream) {
+  if (c && c->loaded && !c->tail_only && in && pidx && logits && B > 0 && B <= c->graph_max_b && !c->stem_ev) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    DevGuard g(c->device);
+    HIP_TRY(c, hipStreamIsCapturing((hipStream_t)stream, &cs));
+    if (cs == hipStreamCaptureStatusNone) return forward_graph(c, in, u8, B, pidx, logits, probs, (hipStream_t)stream);
+  }
+  return forward_impl(c, in, u8, B, pidx, logits, probs, stream);
+}
+
 }  // namespace
 
 extern "C" {
@@ -701,6 +814,7 @@ int fac_create(int device, int dtype, fac_ctx** out) {
 int fac_load_weights(fac_ctx* c, const fac_tensor_desc* descs, int n) {
   if (!c || !descs || n <= 0) return set_err(c, FAC_ERR_ARG, "bad load arguments");
   DevGuard g(c->device);
+  drop_graphs(c);
   for (void* p : c->weights) (void)hipFree(p);
   c->weights.clear();
   c->loaded = false;
@@ -722,6 +836,8 @@ int fac_workspace_bytes(fac_ctx* c, int B, size_t* out) {
 int fac_set_stem_chunk(fac_ctx* c, int crops) {
   if (!c || crops < 0) return FAC_ERR_ARG;
   if (crops != c->stem_chunk) {
+    DevGuard g(c->device);
+    drop_graphs(c);
     c->stem_chunk = crops;
     const int cap = c->cap_B;
     c->cap_B = 0;  // force re-layout on next use
@@ -736,7 +852,16 @@ int fac_set_stem_chunk(fac_ctx* c, int crops) {
 int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (!c || !key) return FAC_ERR_ARG;
   const std::string k(key);
+  {  // every knob can change what a captured forward would launch
+    DevGuard g(c->device);
+    drop_graphs(c);
+  }
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
+  if (k == "graph_max_b") {
+    if (value < 0 || value > 256) return set_err(c, FAC_ERR_ARG, "graph_max_b must be 0..256");
+    c->graph_max_b = value;
+    return FAC_OK;
+  }
   if (k == "tail_only") {
     if (c->loaded) return set_err(c, FAC_ERR_ARG, "tail_only must be set before fac_load_weights");
     c->tail_only = value != 0;
@@ -749,14 +874,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "stem_events") {
     c->stem_ev = value != 0;
     c->stem_ev_used = 0;
-    return FAC_OK;
-  }
-  if (k == "fuse45") {  // 1: conv4 -> conv5 fused (conv45_fused); 0 (default): two launches
-    c->fuse45 = value != 0;
-    return FAC_OK;
-  }
-  if (k == "conv_db") {  // 1 (default): conv3x3_db for the 28^2 tiles; 0: the LDS weight ring (A/B); process-wide
-    fac::set_conv_db(value);
     return FAC_OK;
   }
   if (k == "nd_occ3") {  // convnd_igemm 3-per-CU tile for cout <= 64 up to this many K steps (default 4; 0 = off); process-wide
@@ -785,10 +902,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   }
   if (k == "pool_win") {  // 1 (default): max pools with a (1,3,3) / (3,3,3) / (2,2,2) window by pool_max_win; 0: pool_nd; process-wide
     fac::set_pool_win(value != 0);
-    return FAC_OK;
-  }
-  if (k == "stem_dynamic") {
-    c->stem_dynamic = value != 0;
     return FAC_OK;
   }
   if (k == "stem_nwg") {
@@ -833,19 +946,28 @@ int fac_forward_features(fac_ctx* c, const void* d_feat, int B, const int32_t* d
   int rc = ensure_ws(c, B);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  for (int i = 0; i < 2; ++i)
-    if (c->tail_pending[i]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[i], 0));
-  return tail_impl(c, (const uint16_t*)d_feat, B, d_pos, d_logits, d_probs, st, nullptr, d_hidden);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_TRY(c, hipStreamIsCapturing(st, &cs));
+  if (cs != hipStreamCaptureStatusNone) {
+    for (int i = 0; i < 2; ++i)
+      if (c->tail_pending[i]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[i], 0));
+    return tail_impl(c, (const uint16_t*)d_feat, B, d_pos, d_logits, d_probs, st, nullptr, d_hidden);
+  }
+  rc = order_on(c, st);  // the shared encoder buffers: after the context's previous forward on any stream
+  if (rc) return rc;
+  rc = tail_impl(c, (const uint16_t*)d_feat, B, d_pos, d_logits, d_probs, st, nullptr, d_hidden);
+  if (rc) return rc;
+  return mark_done(c, st);
 }
 
 int fac_forward_nchw_f32(fac_ctx* c, const float* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,
                          void* stream) {
-  return forward_impl(c, d_in, false, B, d_pos, d_logits, d_probs, stream);
+  return forward_entry(c, d_in, false, B, d_pos, d_logits, d_probs, stream);
 }
 
 int fac_forward_nhwc_u8(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits, float* d_probs,
                         void* stream) {
-  return forward_impl(c, d_in, true, B, d_pos, d_logits, d_probs, stream);
+  return forward_entry(c, d_in, true, B, d_pos, d_logits, d_probs, stream);
 }
 
 int fac_forward_nhwc_u8_pipelined(fac_ctx* c, const uint8_t* d_in, int B, const int32_t* d_pos, float* d_logits,
@@ -1006,6 +1128,12 @@ void fac_destroy(fac_ctx* c) {
     }
     for (hipEvent_t e : c->stem_evs) (void)hipEventDestroy(e);
     if (c->ev_stack) (void)hipEventDestroy(c->ev_stack);
+    drop_graphs(c);
+    if (c->cap_st) (void)hipStreamDestroy(c->cap_st);
+    for (void* p : c->g_in)
+      if (p) (void)hipFree(p);
+    if (c->g_pidx) (void)hipFree(c->g_pidx);
+    if (c->g_out) (void)hipFree(c->g_out);
     for (void* p : c->weights) (void)hipFree(p);
     if (c->ws) (void)hipFree(c->ws);
     if (c->err_host) (void)hipHostFree(c->err_host);

@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256) void pool_max_win(fac_pool_desc p, int total) 
 // three, bit-identical (a max selects one of its inputs either way).
 // zg: output frames per thread (all of them by default).  Round 3 tried
 // 1 / 2 / 4 of S3D's 8 frames per thread for more parallelism: the whole
-// S3D step got 9 / 4 / 1 % slower (same box, tools/pool_ab.sh): the frame
+// S3D step got 9 / 4 / 1 % slower (same box, tools/archive/pool_ab.sh): the frame
 // walk's reuse of the frame maxima, not latency, is what counts.
 template <class T>
 __global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total, int zg) {
@@ -592,7 +592,7 @@ __global__ __launch_bounds__(256) void maxpool3_s1(fac_pool_desc p, int total, i
 // ---- maxpool3_roll (round 4): the same MaxPool3d(3, 1, 1) for 7-wide maps
 // (S3D's 4x7x7 Inception blocks), with three loads per output instead of
 // nine: 61.5-65.8 -> 33.6-35.2 us per call at 384 clips, bf16
-// (tools/pool_roll_ab.py; on the 8x14x14 maps the W = 14 instance was no
+// (tools/archive/pool_roll_ab.py; on the 8x14x14 maps the W = 14 instance was no
 // faster than maxpool3_s1 at 2 waves per SIMD: 200 / 300 vs 225 / 287 us).  One thread per (clip,
 // frame group, row y, 8-channel piece) walks a whole row of W positions
 // (compile time, fully unrolled) through the frames: per input frame the

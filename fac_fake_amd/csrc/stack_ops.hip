@@ -24,7 +24,7 @@ hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, co
                           bool relu);
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
-                          hipStream_t s, int* sched = nullptr);
+                          hipStream_t s);
 
 static inline uint16_t to16(int dtype, float f) {
   return dtype == 0 ? fac_host::f32_to_bf16(f) : fac_host::f32_to_f16(f);

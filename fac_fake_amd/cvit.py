@@ -69,6 +69,19 @@ def reference_mask_poisons(mask, B: int, heads: int = 8, n_tokens: int = 2) -> b
     return bool(torch.isinf(dots).any())
 
 
+_SLOTS: dict = {}
+
+
+def _default_slots(device) -> torch.Tensor:
+    """int32 arange(32) on `device`, made once: the default slots 0..B-1 of a
+    B <= 32 call (cvit.py:175) as a slice, with no per-call launch or copy."""
+    device = torch.device(device)
+    t = _SLOTS.get(device)
+    if t is None:
+        t = _SLOTS[device] = torch.arange(MAX_SLOTS, dtype=torch.int32, device=device)
+    return t
+
+
 class _Node(nn.Module):
     """Parameter container (keeps state_dict paths such as features.1.running_var)."""
 
@@ -122,8 +135,11 @@ class CViT(nn.Module):
         self._ctx_device = None
         self._loaded_versions = None
         # one fac_ctx per model: its workspace and streams are shared by every
-        # call, and the C ABI leaves serialising calls to the caller
-        # (include/fac_cvit.h), so threads sharing the model take this lock
+        # call.  The C ABI orders the forwards of one context on the device
+        # (each waits for the previous one's last kernel, whatever stream
+        # either ran on), and this lock serialises the host side of the calls
+        # (the context's bookkeeping is not thread-safe), so threads may share
+        # the model on different streams.
         self._lock = threading.RLock()
         self.eval()
 
@@ -220,7 +236,7 @@ class CViT(nn.Module):
                 # what `x += self.pos_embedding[0:B]` raises in the reference (cvit.py:175)
                 raise RuntimeError(f"The size of tensor a ({B}) must match the size of tensor b ({MAX_SLOTS}) "
                                    f"at non-singleton dimension 0")
-            return torch.arange(B, dtype=torch.int32, device=device)
+            return _default_slots(device)[:B]
         p = torch.as_tensor(pos_index)
         if p.shape != (B,):
             raise ValueError(f"pos_index must have shape ({B},), got {tuple(p.shape)}")

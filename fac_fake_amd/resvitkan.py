@@ -184,7 +184,7 @@ class ResVitKan(nn.Module):
     # keep a block's activations in the Infinity Cache, but measured on MI355X
     # (B = 256, bf16) the whole batch is fastest: 8.9 ms vs 9.5 / 11.0 / 15.6
     # ms at 128 / 64 / 32 — the layers are not HBM-bound, the smaller grids
-    # just fill the 256 CUs worse (tools/rvk_chunks.sh)
+    # just fill the 256 CUs worse (tools/archive/rvk_chunks.sh)
     feature_chunk = 0
     # a layer1 bottleneck's conv3 and the next block's conv1 run as one launch
     # (fac_bottleneck_pw2).  Layer2's pairs stay two launches: the fused

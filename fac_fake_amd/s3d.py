@@ -163,7 +163,7 @@ class S3D(nn.Module):
                 # 128 (zero rows of the (1,3,3) half): that half then has a
                 # conv.hip tile and the (3,1,1) half reads a uniform-tap K
                 # (convnd_pt with a partial column block). Mixed_3c, 384 clips:
-                # 327 -> 160 us (tools/s3d_small_ab.py); 32 -> 64 is slower
+                # 327 -> 160 us (tools/archive/s3d_small_ab.py); 32 -> 64 is slower
                 m2w = (b2b + 127) // 128 * 128 if b2b > 64 and b2b % 64 else None
                 b1, b2 = sep(f"{p}.branch1.1", 3, 1, 1), sep(f"{p}.branch2.1", 3, 1, 1, mid_pad=m2w)
 
@@ -273,11 +273,16 @@ class S3D(nn.Module):
             return pack_input(x.float(), dtype=self.dtype_name, u8=False, spatial=(T, H, W))
         # base.0's space-to-depth cells are made inside its conv (ops.conv_s2d4_clip);
         # a uint8 clip (decoded frames: the reference's values before its float
-        # cast, S3D-test.py:94-96) is read as is, a quarter of the bytes
-        if x.dtype == torch.uint8 and _lib.exports("fac_conv_s2d4_clip_u8"):
-            return x.contiguous()
-        if _lib.exports("fac_conv_s2d4_clip"):
-            return x.float().contiguous()
+        # cast, S3D-test.py:94-96) is read as is, a quarter of the bytes.  That
+        # kernel tiles the output in 8 x 28 boxes of the half-resolution map
+        # (H % 16 == 0, W % 56 == 0, e.g. 112 x 112 or 224 x 224); any other
+        # size (the reference takes any: avg_pool3d runs over the full map,
+        # model.py:43) gets packed cells and base.0 runs on the generic conv.
+        if H % 16 == 0 and W % 56 == 0:
+            if x.dtype == torch.uint8 and _lib.exports("fac_conv_s2d4_clip_u8"):
+                return x.contiguous()
+            if _lib.exports("fac_conv_s2d4_clip"):
+                return x.float().contiguous()
         return pack_input_s2d(x.float(), dtype=self.dtype_name, u8=False, pad_before=2, pad_after=1)
 
     def base_outputs(self, x: torch.Tensor) -> list:

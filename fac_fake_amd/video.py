@@ -105,15 +105,16 @@ def reference_boxes(boxes, length: int) -> np.ndarray:
     """The boxes the reference would crop: per frame read (frame_indices), that
     frame's first 5 faces, until 29 crops (cvit_prediction.py:107-121,189-196)."""
     boxes = np.asarray(boxes, dtype=np.int32).reshape(-1, 5)
-    per_frame = {}
-    for bx in boxes:
-        per_frame.setdefault(int(bx[0]), []).append(bx)
-    out = []
-    for f in frame_indices(length):
-        for bx in per_frame.get(f, [])[:FACES_PER_FRAME]:
-            if len(out) < MAX_CROPS_REFERENCE:
-                out.append(bx)
-    return np.asarray(out, dtype=np.int32).reshape(-1, 5)
+    # each frame's first FACES_PER_FRAME boxes, in list order (a stable sort
+    # by frame keeps it), located by binary search per frame read
+    order = np.argsort(boxes[:, 0], kind="stable")
+    by_frame = boxes[order]
+    fi = np.asarray(frame_indices(length), dtype=np.int64)
+    lo = np.searchsorted(by_frame[:, 0], fi, "left")
+    cnt = np.minimum(np.searchsorted(by_frame[:, 0], fi, "right") - lo, FACES_PER_FRAME)
+    start = np.repeat(lo - (np.cumsum(cnt) - cnt), cnt)   # row of the k-th crop = its read's lo + rank
+    idx = (start + np.arange(int(cnt.sum())))[:MAX_CROPS_REFERENCE]
+    return by_frame[idx].astype(np.int32).reshape(-1, 5)
 
 
 def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", group=None,
@@ -134,8 +135,11 @@ def predict_video(model, frames: torch.Tensor, boxes, mode: str = "reference", g
         if not (isinstance(fr, torch.Tensor) and fr.is_cuda):
             fr = torch.as_tensor(np.ascontiguousarray(fr)).to(_work_device(frames))
         crops = crop_faces(fr, sel)
+        # <= 29 crops: one chunk, slots 0..n-1 = the model's default slots
+        # (cached on the device: no host->device copy per video)
+        slots = None if len(sel) <= 32 else torch.from_numpy(chunk_slots(len(sel)))
         with torch.no_grad():
-            logits = model.forward_u8(crops, pos_index=torch.from_numpy(chunk_slots(len(sel))))
+            logits = model.forward_u8(crops, pos_index=slots)
     elif mode == "dense":
         boxes = np.asarray(boxes, dtype=np.int32).reshape(-1, 5)
         n = len(boxes)

@@ -79,7 +79,16 @@ int fac_forward_nchw_f32(fac_ctx* ctx, const float* d_in, int B, const int32_t* 
 
 /* Same, from raw uint8 NHWC face crops [B,224,224,3] (RGB, the crop format of
  * cvit_prediction.py:106-121,202): the /255 + ImageNet normalisation of
- * cvit_prediction.py:41-45,212-215 is fused into conv1. */
+ * cvit_prediction.py:41-45,212-215 is fused into conv1.
+ * Both forwards: with B <= the "graph_max_b" option (default 32, which covers
+ * the reference's one-video call of <= 29 crops, cvit_prediction.py:224-229)
+ * on a stream that is not being captured, the forward replays a hipGraph
+ * captured once per (B, input kind, d_probs != NULL): d_in and d_pos_index are
+ * copied into context-owned buffers, the graph runs, the outputs are copied
+ * out -- one graph launch instead of ~60 kernel launches, bit-identical
+ * outputs.  Graphs are dropped on fac_load_weights, fac_set_option and
+ * workspace growth.  Calls on one context from different streams are ordered
+ * on the device (each waits for the context's previous forward). */
 int fac_forward_nhwc_u8(fac_ctx* ctx, const uint8_t* d_in, int B, const int32_t* d_pos_index, float* d_logits,
                         float* d_probs, void* stream);
 
@@ -147,7 +156,8 @@ int fac_stem_event_ms(fac_ctx* ctx, float* avg_ms, int* n_launches);
  * an error) and raises a host-visible flag; the context's NEXT forward call
  * (fac_forward_*, fac_forward_features, pipelined) then returns FAC_ERR_ARG
  * before enqueueing anything and clears the flag; fac_last_error names the
- * offending forward by its call number on the context.  fac_check_device_errors
+ * offending forward by its encoder-launch number on the context (one per
+ * batch; a graph replay reports the number of its capture).  fac_check_device_errors
  * reads (and clears) the flag after synchronising the device: 0, or the call
  * number (>= 1) of a forward since the last check that saw such an index.  Not for use inside graph
  * capture (a captured forward's flag is seen by the first eager call after
@@ -186,18 +196,12 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * "gemm_head" (GEMM tile variant -1..3 per call site), "proj_splits" (split-K
  * of to_out and FF2: 1, 2 or 4), "tail_only" (before fac_load_weights: no
  * conv stem, fac_forward_features only), "tail_priority", "stem_events" (1 =
- * time every fused-stem launch, fac_stem_event_ms), "stem_dynamic" (1 =
- * the fused stem claims boxes from a device counter; 0 = static box
- * schedule, the default), "stem_nwg" (persistent fused-stem workgroups; 0 = one per
- * CU, the default), "ffn_ln_eps_exp" (n:
+ * time every fused-stem launch, fac_stem_event_ms), "stem_nwg" (persistent
+ * fused-stem workgroups; 0 = one per CU, the default), "ffn_ln_eps_exp" (n:
  * the FeedForward PreNorm LayerNorm uses eps = 10^-n; default 5, the RepBn8
- * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48), "conv_db" (1 = the
- * 28x28 3x3 convs fetch their weight fragments straight into registers,
- * conv3x3_db, the default; 0 = through the LDS weight ring; bit-identical
- * outputs; process-wide, for A/B measurements), "fuse45" (1 = conv4 -> conv5
- * as one kernel, conv4 recomputed on each box's halo in LDS; 0 = two
- * launches, the default: the fused kernel measured neutral, DESIGN.md §3.4;
- * bit-identical outputs).  Process-wide knobs of the fac_ops.h layer kernels
+ * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48),
+ * "graph_max_b" (forwards of B <= n crops replay a captured hipGraph, see
+ * fac_forward_nhwc_u8; default 32, 0 = always eager).  Process-wide knobs of the fac_ops.h layer kernels
  * (A/B measurements; any context sets them): "nd_pt_wide" (n >= 0: convnd_pt
  * also takes uniform-tap convs whose cout is not a multiple of 128, and
  * fac_conv_nd_split's column segments, from n 256-row tiles on; default 32,

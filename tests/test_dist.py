@@ -51,3 +51,37 @@ def test_sharded_gather_matches_single_process(golden, world, n):
     for rank, full, score in res:
         assert np.array_equal(full, logits)
         assert score == pytest.approx(want, abs=1e-7)
+
+
+def _bench_dist_check(gpus: int):
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["FAC_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", str(gpus), "--dist-check"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout      # only rank 0 prints
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_its_own_ranks():
+    """VERDICT r04 missing #2: `bench.py --gpus 2` without torchrun starts the
+    two ranks itself (fresh child processes, rendezvous on 127.0.0.1) and
+    the process group sees both."""
+    out = _bench_dist_check(2)
+    assert out["n_gpus"] == 2
+    ln = out["launch"]
+    assert ln["world_size"] == 2 and ln["ranks_seen"] == [0, 1] and ln["local_ranks"] == [0, 1]
+    assert ln["backend"] == "gloo" and ln["launcher"].startswith("bench.py")
+
+
+def test_bench_single_rank_unchanged():
+    out = _bench_dist_check(1)
+    assert out["n_gpus"] == 1
+    assert out["launch"]["world_size"] == 1 and out["launch"]["launcher"] == "single process"

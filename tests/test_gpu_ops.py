@@ -664,6 +664,32 @@ def test_s3d_matches_emulation_tightly(s3d_models, golden):
     assert (lg.cpu() - ref).abs().max() <= 2e-3
 
 
+@pytest.mark.parametrize("hw", [(128, 128), (96, 160), (112, 56)])
+def test_s3d_clip_sizes_outside_the_fused_tiling(s3d_models, hw):
+    """base.0's fused s2d conv (fac_conv_s2d4_clip) tiles H % 16,
+    W % 56; other clip sizes (the reference takes any, model.py:43) take the
+    packed-cell route on the generic conv.  (112, 56) is on the fused route
+    at a width the bench never uses.  fp16 vs the oracle's emulation of the
+    HIP rounding points (logits within 2e-3, as the 112^2 test) and the fp32
+    oracle within the 1e-3 probability bar; a uint8 clip gives the same
+    logits as its float copy."""
+    from oracle import s3d_torch as O
+    from fac_fake_amd.weights import make_s3d_state_dict, s3d_clips_varied
+    h, w = hw
+    x = torch.from_numpy(s3d_clips_varied(2, 16, max(h, w), seed=7))[..., :h, :w].contiguous()
+    sd = make_s3d_state_dict(0, 1, False)
+    m = s3d_models[("no", "fp16")]
+    lg, pr = m(x.to(DEV), return_probs=True)
+    lg8 = m(x.to(torch.uint8).to(DEV))
+    torch.cuda.synchronize()
+    emu = O.forward_emulated(sd, x, False, "fp16")
+    ref = O.forward_fp32(sd, x, False)
+    assert lg.shape == (2, 1) and torch.isfinite(lg).all()
+    assert (lg.cpu() - emu).abs().max() <= 2e-3, (lg.cpu(), emu)
+    assert (pr.cpu().double() - torch.sigmoid(ref.double())).abs().max() <= 1e-3
+    assert torch.equal(lg8, lg)
+
+
 def test_s3d_graph_replay_matches_eager(s3d_models):
     from fac_fake_amd.weights import s3d_clips
     m = s3d_models[("yes", "bf16")]

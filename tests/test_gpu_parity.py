@@ -189,37 +189,6 @@ def test_fused_stem224_vs_unfused_and_oracle(models, sd, dt, torch_threads):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_conv45_fused_equals_unfused(models, dt):
-    """conv4 -> conv5 as one kernel (option fuse45, off by default: measured
-    neutral; conv45_fused: conv4 recomputed on each
-    box's 18x18 halo in LDS, rounded to 16 bits exactly where the unfused
-    path stores it, then conv5 with the same k order): conv5's output, the
-    stem's output and the logits are bit-identical to the two-launch path,
-    on crops whose boxes cover every image border (n = 7: 343 boxes)."""
-    from fac_fake_amd import _lib
-    lib = _lib.load()
-    m = models[dt]
-    n = 7
-    x = torch.from_numpy(make_crops(n, seed=45)).to(DEV)
-    tdt = torch.float16 if dt == "fp16" else torch.bfloat16
-    pidx = (torch.arange(n, device=DEV) % 32).to(torch.int32)
-    outs = {}
-    for fuse in (1, 0):
-        _lib.check(lib.fac_set_option(m._ctx, b"fuse45", fuse), m._ctx, "opt")
-        c5 = torch.empty(n, 112, 112, 64, dtype=tdt, device=DEV)
-        _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), n, 4, c5.data_ptr(), None), m._ctx, "dbg")
-        st = torch.empty(n, 7, 7, 512, dtype=tdt, device=DEV)
-        _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), n, 16, st.data_ptr(), None), m._ctx, "dbg")
-        with torch.no_grad():
-            lg = m.forward_u8(x, pos_index=pidx)
-        torch.cuda.synchronize()
-        outs[fuse] = (c5.view(torch.int16).cpu(), st.view(torch.int16).cpu(), lg.cpu())
-    _lib.check(lib.fac_set_option(m._ctx, b"fuse45", 0), m._ctx, "opt")
-    for a, b in zip(outs[1], outs[0]):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("dt", ["fp16", "bf16"])
 def test_tail_isolated(models, sd, dt, torch_threads):
     """Patch embedding + 6 transformer layers + head from the oracle's stem
     output: within the 16-bit rounding envelope of the fp32 tail."""
@@ -330,19 +299,31 @@ def test_out_of_range_pos_index_is_an_error_at_the_c_abi(models):
     good = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device=DEV)
     bad = torch.tensor([0, 1, 40, 3], dtype=torch.int32, device=DEV)
     st = torch.cuda.current_stream().cuda_stream
+    # eager forwards (the small-batch graph replay bakes in its capture's
+    # number; covered below)
+    m.set_option("graph_max_b", 0)
+    try:
+        assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
+        torch.cuda.synchronize()
+        rc = lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st)
+        msg = lib.fac_last_error(ctx)
+        # the error names the offending forward: launch #n, the next #n+1
+        import re
+        got = re.search(rb"encoder launch #(\d+) of this context \(the next is #(\d+)", msg)
+        assert rc == -1 and b"pos_index" in msg and got and int(got.group(2)) == int(got.group(1)) + 1, msg
+        assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0  # cleared
+        assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
+        flags = ctypes.c_int()
+        assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == int(got.group(1)) + 2
+        assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == 0
+        assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0
+        torch.cuda.synchronize()
+    finally:
+        m.set_option("graph_max_b", 32)
+    # the graph replay path raises the same flag and the next call is refused
     assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
     torch.cuda.synchronize()
-    rc = lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st)
-    msg = lib.fac_last_error(ctx)
-    # the error names the offending forward: call #n, and this one #n+1
-    import re
-    got = re.search(rb"forward call #(\d+) of this context \(this call is #(\d+)\)", msg)
-    assert rc == -1 and b"pos_index" in msg and got and int(got.group(2)) == int(got.group(1)) + 1, msg
-    assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0  # cleared
-    assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, bad.data_ptr(), lg.data_ptr(), None, st) == 0
-    flags = ctypes.c_int()
-    assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == int(got.group(1)) + 2
-    assert lib.fac_check_device_errors(ctx, ctypes.byref(flags)) == 0 and flags.value == 0
+    assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == -1
     assert lib.fac_forward_nhwc_u8(ctx, x.data_ptr(), 4, good.data_ptr(), lg.data_ptr(), None, st) == 0
     torch.cuda.synchronize()
 
@@ -610,17 +591,16 @@ def test_host_frames_upload_only_what_is_cropped(models, mode):
 
 @pytest.mark.parametrize("cin,cout,pool", [(128, 256, 0), (256, 256, 1), (96, 192, 0), (160, 128, 1), (32, 128, 0)])
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
-def test_conv_db_tile_equals_weight_ring(models, cin, cout, pool, dt):
-    """The 28x28 3x3 convs default to conv3x3_db (weight fragments straight
-    into registers, register-staged halo, one barrier per 32-channel chunk).
-    Same k order and MFMA sequence as conv3x3_bn_relu (LDS weight ring), so
-    the outputs are bit-identical, for every 28^2 column tile (BN 256 / 192 /
-    128: CViT, S3D, ResNet), odd and even chunk counts, a single chunk,
-    ragged batch, and with the fused 2x2 max-pool."""
+def test_conv_db_tile_vs_torch_fp32(models, cin, cout, pool, dt):
+    """The 28x28 3x3 convs run on conv3x3_db (weight fragments straight into
+    registers, register-staged halo, one barrier per 32-channel chunk; its
+    LDS-weight-ring twin lost twice and was removed in round 5): every 28^2
+    column tile (BN 256 / 192 / 128: CViT, S3D, ResNet), odd and even chunk
+    counts, a single chunk, ragged batch, and the fused 2x2 max-pool, against
+    torch's fp32 conv of the same 16-bit operands (two 16-bit ulps)."""
     from fac_fake_amd import _lib
     from fac_fake_amd.ops import TORCH16, _zero256
     lib = _lib.load()
-    m = models[dt]
     g = torch.Generator().manual_seed(cin + cout + pool)
     n = 5
     x = torch.randn(n, 28, 28, cin, generator=g).relu().to(TORCH16[dt]).to(DEV)
@@ -632,14 +612,12 @@ def test_conv_db_tile_equals_weight_ring(models, cin, cout, pool, dt):
     pk = pk.to(DEV)
     ho = 14 if pool else 28
     outs = []
-    for db in (1, 0):
-        m.set_option("conv_db", db)
+    for _ in range(2):   # and run to run: bit-identical
         y = torch.empty(n, ho, ho, cout, dtype=TORCH16[dt], device=DEV)
         _lib.check(lib.fac_conv3x3(_lib.DTYPES[dt], x.data_ptr(), pk.data_ptr(), b.data_ptr(), y.data_ptr(), n, 28,
                                    cin, cout, pool, 1, _zero256(x.device).data_ptr(),
                                    torch.cuda.current_stream().cuda_stream), None, "fac_conv3x3")
         outs.append(y)
-    m.set_option("conv_db", 1)
     torch.cuda.synchronize()
     assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
     ref = torch.nn.functional.conv2d(x.cpu().float().permute(0, 3, 1, 2), w.to(TORCH16[dt]).float(), b.cpu(),
@@ -678,3 +656,81 @@ def test_stem_event_timing(models):
     finally:
         m.set_option("stem_events", 0)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_small_batch_graph_replay_is_bit_identical(models, dt):
+    """forwards of B <= 32 crops (the reference's one-video
+    call, cvit_prediction.py:224-229) replay a hipGraph captured per (B,
+    input kind, probs).  Logits and probabilities are bit-identical to the
+    eager forward (option graph_max_b = 0), for uint8 and fp32 NCHW input,
+    interleaved batch sizes (graph cache hits and misses), explicit slots,
+    and after new weights are loaded (the graphs are dropped and recaptured)."""
+    from oracle.cvit_torch import normalize_u8
+    m = models[dt]
+    cases = [(1, 3), (29, 4), (7, 5), (29, 6), (32, 7), (1, 8)]
+    got = []
+    for B, seed in cases:
+        u8 = make_crops(B, seed=seed)
+        x = torch.from_numpy(u8).to(DEV)
+        pidx = torch.from_numpy((np.arange(B) * 7 % 32).astype(np.int32))
+        lg, pr = m.forward_u8(x, return_probs=True)
+        lg2 = m.forward_u8(x, pos_index=pidx)
+        lg3 = m(normalize_u8(u8).to(DEV)) if B <= 8 else None
+        got.append((lg.clone(), pr.clone(), lg2.clone(), None if lg3 is None else lg3.clone()))
+    m.set_option("graph_max_b", 0)
+    try:
+        for (B, seed), g in zip(cases, got):
+            u8 = make_crops(B, seed=seed)
+            x = torch.from_numpy(u8).to(DEV)
+            pidx = torch.from_numpy((np.arange(B) * 7 % 32).astype(np.int32))
+            lg, pr = m.forward_u8(x, return_probs=True)
+            assert torch.equal(g[0], lg) and torch.equal(g[1], pr), B
+            assert torch.equal(g[2], m.forward_u8(x, pos_index=pidx)), B
+            if g[3] is not None:
+                assert torch.equal(g[3], m(normalize_u8(u8).to(DEV))), B
+    finally:
+        m.set_option("graph_max_b", 32)
+    torch.cuda.synchronize()
+
+
+def test_small_batch_graph_follows_new_weights(sd):
+    """Loading a different state_dict drops the captured graphs: the replay
+    then matches the eager forward on the new weights."""
+    from fac_fake_amd.cvit import CViT
+    from fac_fake_amd.weights import make_state_dict
+    m = CViT(dtype="fp16")
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    x = torch.from_numpy(make_crops(5, seed=9)).to(DEV)
+    a = m.forward_u8(x).clone()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_state_dict(1).items()})
+    b = m.forward_u8(x).clone()
+    m.set_option("graph_max_b", 0)
+    c = m.forward_u8(x)
+    torch.cuda.synchronize()
+    assert not torch.equal(a, b) and torch.equal(b, c)
+    m._release()
+
+
+def test_forwards_on_two_streams_are_ordered(models):
+    """calls on one context from different streams share its
+    workspace; the C ABI makes each forward wait for the previous one on the
+    device.  Two streams, no host sync between the calls, eager (B = 40) and
+    graph (B = 20) paths: every result equals the same call made alone."""
+    m = models["fp16"]
+    xs = [torch.from_numpy(make_crops(n, seed=30 + n)).to(DEV) for n in (40, 20, 40, 20)]
+    pos = [(torch.arange(x.shape[0]) % 32).to(torch.int32) for x in xs]   # host slots: no device sync
+    alone = []
+    for x, p in zip(xs, pos):
+        alone.append(m.forward_u8(x, pos_index=p).clone())
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)]
+    outs = []
+    for i, (x, p) in enumerate(zip(xs, pos)):
+        s = streams[i & 1]
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            outs.append(m.forward_u8(x, pos_index=p))
+    torch.cuda.synchronize()
+    for a, b in zip(alone, outs):
+        assert torch.equal(a, b)

@@ -1,4 +1,4 @@
-"""Per-layer SQ counter table from tools/conv_pmc.sh output (gpurun_out/cpmc)."""
+"""Per-layer SQ counter table from tools/archive/conv_pmc.sh output (gpurun_out/cpmc)."""
 import collections
 import csv
 import glob

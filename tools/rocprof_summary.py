@@ -1,4 +1,4 @@
-"""Turn rocprofv3 CSVs (tools/profile.sh output) into the committed summaries.
+"""Turn rocprofv3 CSVs (tools/archive/profile.sh output) into the committed summaries.
 
     python tools/rocprof_summary.py gpurun_out/prof profiles/r01
 
@@ -8,7 +8,7 @@ writes
   <prefix>_traffic.json       per-kernel mean HBM bytes per dispatch from the
                               FETCH_SIZE and WRITE_SIZE passes (separate runs)
   <prefix>_pmc.json           per-kernel / per-stage SQ counters (pmc1, pmc2
-                              passes of tools/profile_r03.sh): MFMA busy
+                              passes of tools/archive/profile_r03.sh): MFMA busy
                               fraction, wave-state split, LDS bank conflicts
 
 MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles),
@@ -154,7 +154,7 @@ def main(src: str, prefix: str):
             durs = stage_durations(tr)
         pmc = {"by_stage": defaultdict(dict), "by_kernel": defaultdict(dict),
                "method": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8); one rocprofv3 run per pass "
-                         "(tools/profile_r03.sh); per-stage = mean over that stage's dispatches"}
+                         "(tools/archive/profile_r03.sh); per-stage = mean over that stage's dispatches"}
         for p in passes:
             if not p.exists():
                 continue
