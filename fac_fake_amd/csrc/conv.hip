@@ -783,9 +783,11 @@ static hipError_t launch_db(const uint16_t* in, const uint16_t* wpk, const float
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                                 int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st,
-                                int relu) {
+                                int relu, int bn) {
   if (W != H) return hipErrorInvalidValue;
-  switch (H * 1000 + conv_block_n(H, Cout)) {
+  if (bn == 0) bn = conv_block_n(H, Cout);
+  if (bn <= 0 || Cout % bn) return hipErrorInvalidValue;
+  switch (H * 1000 + bn) {
     case 224032: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
     // conv4-6 886 -> 769 us vs two halo buffers at 2 per CU)
@@ -814,11 +816,14 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
   return hipGetLastError();
 }
 
+// bn: the output-channel block (0 = conv_block_n's; the weights must be
+// packed for the same block, pack_conv3x3).  Every block gives bit-identical
+// outputs (same k order per output channel).
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st,
-                          bool relu) {
-  if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu);
-  return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu);
+                          bool relu, int bn) {
+  if (dtype == 0) return launch_conv_t<BF16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu, bn);
+  return launch_conv_t<F16>(in, wpk, bias, out, B, H, W, Cin, Cout, pool, zero16, st, relu, bn);
 }
 
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,

@@ -23,15 +23,17 @@
 namespace fac {
 int conv_block_n(int H, int cout);
 void set_nd_pt_wide(int v);
+void set_gemm_small(int max_m, int variant);
 void set_nd_occ3(int v);
 void set_pool_roll(int v);
 void set_pool_win(int v);
 void set_pool3_zg(int v);
 void set_pool_lds14(int v);
-void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out);
+void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out, int bn = 0);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
-                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, bool relu = true);
+                          int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, bool relu = true,
+                          int bn = 0);
 hipError_t launch_conv1(int dtype, bool u8, const void* in, const uint16_t* w1, const float* bias, uint16_t* out,
                         int B, int H, int W, hipStream_t st);
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
@@ -74,6 +76,11 @@ struct ConvLayer {
   bool pool = false;
   uint16_t* w = nullptr;
   float* b = nullptr;
+  // the 28^2 / 14^2 layers also packed for half the output-channel block
+  // (bn_small), taken when the default grid leaves CUs idle (few crops: the
+  // reference's one-video call); bit-identical outputs
+  int bn_small = 0;
+  uint16_t* w_small = nullptr;
 };
 
 struct TLayer {
@@ -179,6 +186,7 @@ struct fac_ctx {
     hipGraphExec_t exec;
   };
   int graph_max_b = 32;
+  int conv_small = 1;  // option "conv_small": 28^2 / 14^2 layers on half-width column blocks when few crops
   std::vector<SmallGraph> graphs;
   hipStream_t cap_st = nullptr;
   void* g_in[2] = {nullptr, nullptr};  // [0] fp32 NCHW, [1] uint8 NHWC; graph_max_b crops each
@@ -226,6 +234,12 @@ int patch_splits(int) { return kPatchSplits; }
 
 hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, uint16_t* out, int B, hipStream_t st) {
   using namespace fac;
+  if (L.w_small && c->conv_small) {
+    const int bn = conv_block_n(L.H, L.Cout), boxes = L.H == 14 ? 1 : (L.H / 4) * (L.H / 28);
+    if ((long long)B * boxes * (L.Cout / bn) < c->num_cu)
+      return launch_conv3x3(c->dtype, in, L.w_small, L.b, out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st, true,
+                            L.bn_small);
+  }
   return launch_conv3x3(c->dtype, in, L.w, L.b, out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st);
 }
 
@@ -424,6 +438,12 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
       std::vector<uint16_t> pk((size_t)co * ci * 9);
       fac::pack_conv3x3(c->dtype, H, ci, co, wfold.data(), pk.data());  // the LDS-image order of conv.hip
       if ((rc = upload(c, pk, &L.w))) return rc;
+      L.bn_small = H == 14 ? 64 : (H == 28 ? 128 : 0);
+      L.w_small = nullptr;
+      if (L.bn_small) {
+        fac::pack_conv3x3(c->dtype, H, ci, co, wfold.data(), pk.data(), L.bn_small);
+        if ((rc = upload(c, pk, &L.w_small))) return rc;
+      }
       if ((rc = upload(c, bf, &L.b))) return rc;
     }
     if (pool_after(i)) H /= 2;
@@ -857,6 +877,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     drop_graphs(c);
   }
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
+  if (k == "conv_small") {
+    c->conv_small = value != 0;
+    return FAC_OK;
+  }
   if (k == "graph_max_b") {
     if (value < 0 || value > 256) return set_err(c, FAC_ERR_ARG, "graph_max_b must be 0..256");
     c->graph_max_b = value;
@@ -912,10 +936,15 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   static const char* gemm_keys[6] = {"gemm_patch", "gemm_qkv", "gemm_out", "gemm_ff1", "gemm_ff2", "gemm_head"};
   for (int i = 0; i < 6; ++i)
     if (k == gemm_keys[i]) {
-      if (value < -1 || value > 3) return set_err(c, FAC_ERR_ARG, "gemm variant must be -1..3");
+      if (value < -1 || value > 6) return set_err(c, FAC_ERR_ARG, "gemm variant must be -1..6");
       c->gemm_var[i] = value;
       return FAC_OK;
     }
+  if (k == "gemm_small") {  // process-wide: tile variant of GEMMs with <= 64 rows (default 5; -1: the wide tiles)
+    if (value < -1 || value > 6) return set_err(c, FAC_ERR_ARG, "gemm_small must be -1..6");
+    fac::set_gemm_small(value < 0 ? 0 : 64, value < 0 ? 0 : value);
+    return FAC_OK;
+  }
   if (k == "ffn_ln_eps_exp") {
     if (value < 1 || value > 12) return set_err(c, FAC_ERR_ARG, "ffn_ln_eps_exp must be 1..12");
     c->ffn_ln_eps = (float)std::pow(10.0, -value);

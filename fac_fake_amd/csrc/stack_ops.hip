@@ -21,7 +21,7 @@ namespace fac {
 int conv_block_n(int H, int cout);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st,
-                          bool relu);
+                          bool relu, int bn = 0);
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
                           hipStream_t s);
@@ -32,9 +32,10 @@ static inline uint16_t to16(int dtype, float f) {
 
 // [n-block][32-channel chunk][tap][q][BN][8]: one tap slice of one chunk is
 // byte-identical to the LDS image conv3x3_bn_relu streams (conv.hip).
-// w: folded fp32 [cout][cin][9].
-void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out) {
-  const int BN = conv_block_n(H, co), CK = 32, nch = ci / CK;
+// w: folded fp32 [cout][cin][9].  bn: the output-channel block (0 =
+// conv_block_n's), as launch_conv3x3 is given it.
+void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out, int bn) {
+  const int BN = bn ? bn : conv_block_n(H, co), CK = 32, nch = ci / CK;
   size_t q = 0;
   for (int nb = 0; nb < co / BN; ++nb)
     for (int ch = 0; ch < nch; ++ch)
@@ -91,7 +92,7 @@ size_t fac_conv3x3_packed_elems(int h, int cin, int cout) {
 int fac_conv3x3_pack(int dtype, int h, int cin, int cout, const float* w, uint16_t* out) {
   if (!w || !out || (dtype != 0 && dtype != 1)) return FAC_ERR_ARG;
   if (!fac::conv3x3_shape_ok(h, cin, cout)) return FAC_ERR_SHAPE;
-  fac::pack_conv3x3(dtype, h, cin, cout, w, out);
+  fac::pack_conv3x3(dtype, h, cin, cout, w, out, 0);
   return FAC_OK;
 }
 

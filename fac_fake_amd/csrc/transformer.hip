@@ -25,7 +25,8 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                    (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
-// C[M][N] = A[M][K] . W[N][K]^T on a BM x 128 output tile (BM = 32 or 64),
+// C[M][N] = A[M][K] . W[N][K]^T on a BM x BN output tile (BM = 32 or 64, BN =
+// 128, or 32 / 64 for the few-row calls: more workgroups streaming W),
 // BK = 64, 4 waves in a WM x (4/WM) grid, each wave FM x FN MFMA 16x16x32
 // tiles.  Both operand tiles go global -> LDS by global_load_lds into an
 // NS-slot ring: tile kt lives in slot kt % NS and is issued NS-1 steps ahead
@@ -37,17 +38,21 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
 // the glds SOURCE address (the LDS side of a glds is lane-linear) and on the
 // fragment read: conflict-free for the ds_read_b128 lane groups.
 // blockIdx.z selects a K range of Kper (split-K; Kper % 64 == 0).
-template <class T, int EPI, int BM, int WM, int NS>
+// Every output's K sum runs in the same order (k-tiles of 64 in sequence, two
+// MFMA k-steps each) for every BM / BN / WM / NS, so the tile variant never
+// changes a result bit: a crop's logits stay independent of its batch.
+template <class T, int EPI, int BM, int WM, int NS, int BN = 128>
 __global__ __launch_bounds__(256, NS <= 3 ? 2 : 1) void gemm_nt(const uint16_t* __restrict__ A, int lda,
                                                                 const uint16_t* __restrict__ Wt, int ldw,
                                                                 const float* __restrict__ bias,
                                                                 void* __restrict__ out_, int ldo, int M, int N,
                                                                 int Kper) {
-  constexpr int BN = 128, BK = 64, WN = 4 / WM;
+  constexpr int BK = 64, WN = 4 / WM;
   constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
   constexpr int SLOT = (BM + BN) * BK;    // elements
   constexpr int GPW = (BM + BN) / 8 / 4;  // glds per wave per tile (8 rows per instruction)
-  static_assert((BM + BN) % 32 == 0 && FM >= 1 && FN >= 1 && NS >= 3, "gemm tile");
+  static_assert((BM + BN) % 32 == 0 && FM >= 1 && FN >= 1 && NS >= 3 && FM * WM * 16 == BM && FN * WN * 16 == BN,
+                "gemm tile");
   __shared__ __attribute__((aligned(16))) uint16_t smem[NS * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -435,8 +440,14 @@ __global__ __launch_bounds__(256) void video_score_seg(const float* __restrict__
 
 namespace fac {
 
-// Tile variants (BM, WM, NS): 0 = 64x128 ring 3 (2 WG/CU), 1 = 64x128 ring 6,
-// 2 = 32x128 ring 3 (2 WG/CU), 3 = 32x128 ring 7.
+// Tile variants (BM x BN, WM, ring NS): 0 = 64x128 ring 3 (2 WG/CU), 1 =
+// 64x128 ring 6, 2 = 32x128 ring 3 (2 WG/CU), 3 = 32x128 ring 7; for few rows
+// (the reference's one-video call: M = 2B <= 58), 4 = 64x32 ring 3, 5 = 64x32
+// ring 6, 6 = 32x64 ring 3.
+constexpr int kGemmVariants = 7;
+constexpr int gemm_bm(int v) { return v == 2 || v == 3 || v == 6 ? 32 : 64; }
+constexpr int gemm_bn(int v) { return v == 4 || v == 5 ? 32 : (v == 6 ? 64 : 128); }
+
 template <class T, int EPI>
 static void launch_gemm_v(int variant, dim3 grid, const uint16_t* A, int lda, const uint16_t* W, int ldw,
                           const float* bias, void* out, int ldo, int M, int N, int Kper, hipStream_t st) {
@@ -444,15 +455,18 @@ static void launch_gemm_v(int variant, dim3 grid, const uint16_t* A, int lda, co
     case 0: gemm_nt<T, EPI, 64, 2, 3><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
     case 1: gemm_nt<T, EPI, 64, 2, 6><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
     case 2: gemm_nt<T, EPI, 32, 1, 3><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
-    default: gemm_nt<T, EPI, 32, 1, 7><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case 3: gemm_nt<T, EPI, 32, 1, 7><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case 4: gemm_nt<T, EPI, 64, 2, 3, 32><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    case 5: gemm_nt<T, EPI, 64, 2, 6, 32><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
+    default: gemm_nt<T, EPI, 32, 1, 3, 64><<<grid, 256, 0, st>>>(A, lda, W, ldw, bias, out, ldo, M, N, Kper); break;
   }
 }
 
 template <class T>
 static hipError_t launch_gemm_t(int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
                                 void* out, int ldo, int M, int N, int K, int splits, int variant, hipStream_t st) {
-  const int bm = variant >= 2 ? 32 : 64;
-  dim3 grid(N / 128, (M + bm - 1) / bm, splits);
+  const int bm = gemm_bm(variant);
+  dim3 grid(N / gemm_bn(variant), (M + bm - 1) / bm, splits);
   const int Kper = K / splits;
   switch (epi) {
     case EPI_F32: launch_gemm_v<T, EPI_F32>(variant, grid, A, lda, W, ldw, bias, out, ldo, M, N, Kper, st); break;
@@ -465,6 +479,15 @@ static hipError_t launch_gemm_t(int epi, const uint16_t* A, int lda, const uint1
   return hipGetLastError();
 }
 
+// Few-row calls (M = 2B rows up to 64: the reference's <= 29-crop video
+// call) default to a narrow tile, so several times more workgroups stream the
+// weights (set_gemm_small; bit-identical to the wide tiles).
+static int kSmallM = 64, kSmallVariant = 5;
+void set_gemm_small(int max_m, int variant) {
+  kSmallM = max_m;
+  kSmallVariant = variant;
+}
+
 // variant < 0: pick by shape.  Measured on MI355X (tools/gemm_sweep.py, bf16,
 // B = 256): the 32x128 / ring-3 tile (2 WG/CU) wins every encoder GEMM
 // (M = 512, K = 1024..2048: QKV 11.1 us, FF1 11.5, FF2/4 7.1, head 8.7 vs
@@ -474,8 +497,8 @@ hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uin
                        void* out, int ldo, int M, int N, int K, int splits, hipStream_t st, int variant) {
   if (N % 128 != 0 || splits < 1 || K % (64 * splits) != 0 || M <= 0 || epi < 0 || epi > EPI_T)
     return hipErrorInvalidValue;
-  if (variant < 0) variant = K / splits >= 1024 && K >= 8192 ? 0 : 2;
-  if (variant > 3) return hipErrorInvalidValue;
+  if (variant < 0) variant = M <= kSmallM ? kSmallVariant : (K / splits >= 1024 && K >= 8192 ? 0 : 2);
+  if (variant >= kGemmVariants) return hipErrorInvalidValue;
   if (dtype == 0) return launch_gemm_t<BF16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, variant, st);
   return launch_gemm_t<F16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, variant, st);
 }

@@ -193,7 +193,7 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
 /* Named knobs: "stem_chunk" (as above), "fuse_stem224" (1 = conv1..conv3 +
  * pool as one fused kernel, the default; 0 = one kernel per conv),
  * "gemm_patch" / "gemm_qkv" / "gemm_out" / "gemm_ff1" / "gemm_ff2" /
- * "gemm_head" (GEMM tile variant -1..3 per call site), "proj_splits" (split-K
+ * "gemm_head" (GEMM tile variant -1..6 per call site), "proj_splits" (split-K
  * of to_out and FF2: 1, 2 or 4), "tail_only" (before fac_load_weights: no
  * conv stem, fac_forward_features only), "tail_priority", "stem_events" (1 =
  * time every fused-stem launch, fac_stem_event_ms), "stem_nwg" (persistent
@@ -201,8 +201,14 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * the FeedForward PreNorm LayerNorm uses eps = 10^-n; default 5, the RepBn8
  * variant's LinearNorm is 6, cvit_GGCA_ADD_DEConv_RepBn8.py:48),
  * "graph_max_b" (forwards of B <= n crops replay a captured hipGraph, see
- * fac_forward_nhwc_u8; default 32, 0 = always eager).  Process-wide knobs of the fac_ops.h layer kernels
- * (A/B measurements; any context sets them): "nd_pt_wide" (n >= 0: convnd_pt
+ * fac_forward_nhwc_u8; default 32, 0 = always eager), "conv_small" (1 = the
+ * 28x28 / 14x14 convs run on half-width output-channel blocks when the
+ * default grid would leave CUs idle, i.e. few crops; the default; 0 = never;
+ * bit-identical outputs).  Process-wide knobs of the fac_ops.h layer kernels
+ * (A/B measurements; any context sets them): "gemm_small" (the GEMM tile
+ * variant 0..6 of calls with <= 64 rows, i.e. forwards of <= 32 crops; default
+ * 5, a 64x32 tile; -1 = the wide tiles; every variant gives bit-identical
+ * results), "nd_pt_wide" (n >= 0: convnd_pt
  * also takes uniform-tap convs whose cout is not a multiple of 128, and
  * fac_conv_nd_split's column segments, from n 256-row tiles on; default 32,
  * 0 = convnd_igemm), "nd_occ3" (convnd_igemm's 3-per-CU 2-slot 128x64 tile

@@ -403,7 +403,7 @@ def test_large_batch_properties(models):
     assert np.array_equal(big[448:], small)     # a crop's logits do not depend on its batch
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
 def test_gemm_variants_vs_torch_fp32(models, dt, variant):
     """Every GEMM tile variant and epilogue vs a torch fp32 matmul of the same
@@ -734,3 +734,48 @@ def test_forwards_on_two_streams_are_ordered(models):
     torch.cuda.synchronize()
     for a, b in zip(alone, outs):
         assert torch.equal(a, b)
+
+
+def test_gemm_tile_variants_are_bit_identical(models):
+    """Every GEMM tile (wide 64/32 x 128 and the narrow few-row 64x32 / 32x64
+    tiles) sums each output's K in the same order: bit-identical outputs, so
+    switching tiles by row count never changes a crop's logits."""
+    m = models["fp16"]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    M, N, K = 58, 3072, 1024
+    a = (torch.randn(M, K, generator=g) * 0.5).to(torch.float16).to(DEV)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.float16).to(DEV)
+    bias = torch.randn(N, generator=g).to(DEV)
+    outs = []
+    for v in range(7):
+        o = torch.empty(M, N, device=DEV)
+        m.debug_gemm(0, a, w, bias, o, splits=1, variant=v)
+        s = torch.empty(4, M, N, device=DEV)
+        m.debug_gemm(4, a, w, bias, s, splits=4, variant=v)
+        outs.append((o, s))
+    torch.cuda.synchronize()
+    for o, s in outs[1:]:
+        assert torch.equal(o, outs[0][0]) and torch.equal(s, outs[0][1])
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_few_crop_forward_equals_full_batch(models, dt):
+    """The reference's one-video call (29 crops) takes the few-row GEMM tiles
+    and the half-width 28^2 / 14^2 conv blocks (fill the CUs at small B); its
+    logits are bit-identical to the same crops scored inside a 256-crop batch
+    (the wide tiles), and to the same call with both switched off."""
+    m = models[dt]
+    crops = make_crops(256, seed=77)
+    pidx = (np.arange(256) % 32).astype(np.int32)
+    big = _run_u8(m, crops, pidx)
+    sel = slice(64, 93)
+    small = _run_u8(m, crops[sel], pidx[sel])
+    assert np.array_equal(big[sel], small)
+    m.set_option("conv_small", 0)
+    m.set_option("gemm_small", -1)
+    try:
+        off = _run_u8(m, crops[sel], pidx[sel])
+    finally:
+        m.set_option("conv_small", 1)
+        m.set_option("gemm_small", 5)
+    assert np.array_equal(off, small)

@@ -71,6 +71,14 @@ def main():
     out[f"forward_u8 B={n} eager (host-timed)"] = timed(lambda: m.forward_u8(crops))
     out[f"forward_u8 B={n} eager (device, back-to-back)"] = device_ms(lambda: m.forward_u8(crops))
     m.set_option("graph_max_b", 32)
+    for gs in (-1, 4, 5, 6):
+        for cs in (0, 1):
+            m.set_option("gemm_small", gs)
+            m.set_option("conv_small", cs)
+            out[f"forward_u8 B={n} graph, gemm_small {gs:2d} conv_small {cs} (device)"] = device_ms(
+                lambda: m.forward_u8(crops))
+    m.set_option("gemm_small", 5)
+    m.set_option("conv_small", 1)
     out["device score + item"] = timed(lambda: video.device_video_score(lg))
     out["predict_video reference"] = timed(lambda: video.predict_video(m, frames, boxes, mode="reference"))
     for k, v in out.items():
