@@ -31,6 +31,10 @@ void set_pool3_zg(int v);
 void set_pool_lds14(int v);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out, int bn = 0);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
+void pack_conv3x3_wino(int dtype, int ci, int co, int bn, const float* w, uint16_t* out);
+hipError_t launch_conv3x3_wino(int dtype, const uint16_t* in, const uint16_t* upk, const float* bias, uint16_t* out,
+                               int B, int H, int Cin, int Cout, int bn, bool pool, const uint16_t* zero16,
+                               hipStream_t st);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, bool relu = true,
                           int bn = 0);
@@ -81,6 +85,8 @@ struct ConvLayer {
   // reference's one-video call); bit-identical outputs
   int bn_small = 0;
   uint16_t* w_small = nullptr;
+  // the 56^2 / 28^2 / 14^2 layers also packed for conv3x3_wino (Winograd F(2,3), wino.hip)
+  uint16_t* w_wino = nullptr;
 };
 
 struct TLayer {
@@ -187,6 +193,7 @@ struct fac_ctx {
   };
   int graph_max_b = 32;
   int conv_small = 1;  // option "conv_small": 28^2 / 14^2 layers on half-width column blocks when few crops
+  int wino = 0;        // option "wino": bit 0 / 1 / 2 = the 14^2 / 28^2 / 56^2 layers as Winograd F(2,3)
   std::vector<SmallGraph> graphs;
   hipStream_t cap_st = nullptr;
   void* g_in[2] = {nullptr, nullptr};  // [0] fp32 NCHW, [1] uint8 NHWC; graph_max_b crops each
@@ -234,6 +241,9 @@ int patch_splits(int) { return kPatchSplits; }
 
 hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, uint16_t* out, int B, hipStream_t st) {
   using namespace fac;
+  const int wbit = L.H == 14 ? 1 : (L.H == 28 ? 2 : (L.H == 56 ? 4 : 0));
+  if (L.w_wino && (c->wino & wbit))
+    return launch_conv3x3_wino(c->dtype, in, L.w_wino, L.b, out, B, L.H, L.Cin, L.Cout, 64, L.pool, c->zero16, st);
   if (L.w_small && c->conv_small) {
     const int bn = conv_block_n(L.H, L.Cout), boxes = L.H == 14 ? 1 : (L.H / 4) * (L.H / 28);
     if ((long long)B * boxes * (L.Cout / bn) < c->num_cu)
@@ -443,6 +453,12 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
       if (L.bn_small) {
         fac::pack_conv3x3(c->dtype, H, ci, co, wfold.data(), pk.data(), L.bn_small);
         if ((rc = upload(c, pk, &L.w_small))) return rc;
+      }
+      L.w_wino = nullptr;
+      if (H <= 56) {
+        std::vector<uint16_t> pw((size_t)co * ci * 12);
+        fac::pack_conv3x3_wino(c->dtype, ci, co, 64, wfold.data(), pw.data());
+        if ((rc = upload(c, pw, &L.w_wino))) return rc;
       }
       if ((rc = upload(c, bf, &L.b))) return rc;
     }
@@ -877,6 +893,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     drop_graphs(c);
   }
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
+  if (k == "wino") {
+    if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "wino must be 0..7 (bit 0: 14^2, 1: 28^2, 2: 56^2)");
+    c->wino = value;
+    return FAC_OK;
+  }
   if (k == "conv_small") {
     c->conv_small = value != 0;
     return FAC_OK;

@@ -132,8 +132,30 @@ def fold_bn(sd, ci, bi):
     return w, b
 
 
+def conv3x3_wino_f23(h: torch.Tensor, w: torch.Tensor, b: torch.Tensor, dtype: str) -> torch.Tensor:
+    """Conv2d(3x3, pad 1) + bias of a 16-bit-valued NCHW input as the HIP
+    path's Winograd F(2,3) along x computes it (fac_fake_amd/csrc/wino.hip):
+    per output pair (2p, 2p+1) and input row, d_x = x-columns 2p-1 .. 2p+2
+    (zero padded), V = (d0-d2, d1+d2, d2-d1, d1-d3) in fp32 rounded to 16
+    bits; U = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2) of each folded kernel row
+    in fp64 rounded to 16 bits; M_j = sum over (channel, kernel row) of
+    U_j V_j in fp32; out = (M0+M1+M2, M1-M2-M3) + bias, fp32 (before ReLU)."""
+    N, C, H, W = h.shape
+    d = F.pad(h.float(), (1, 1, 1, 1)).unfold(3, 4, 2)          # [N, C, H+2, W/2, 4]
+    d0, d1, d2, d3 = d.unbind(-1)
+    V = round_to(torch.stack([d0 - d2, d1 + d2, d2 - d1, d1 - d3], -1), dtype)   # [N, C, H+2, W/2, 4]
+    g = w.double()
+    g0, g1, g2 = g[..., 0], g[..., 1], g[..., 2]                 # [K, C, 3(ky)]
+    U = round_to(torch.stack([g0, (g0 + g1 + g2) * 0.5, (g0 - g1 + g2) * 0.5, g2], -1).float(), dtype)
+    M = sum(torch.einsum("kcj,ncypj->nkypj", U[:, :, ky], V[:, :, ky:ky + H]) for ky in range(3))
+    m0, m1, m2, m3 = M.unbind(-1)                                # [N, K, H, W/2]
+    out = torch.stack([m0 + m1 + m2, m1 - m2 - m3], -1).reshape(N, -1, H, W)
+    return out + b.view(1, -1, 1, 1)
+
+
 @torch.no_grad()
-def forward_emulated(sd, img: torch.Tensor, pos_index=None, dtype: str = "bf16", return_features: bool = False):
+def forward_emulated(sd, img: torch.Tensor, pos_index=None, dtype: str = "bf16", return_features: bool = False,
+                     wino=()):
     """The gfx950 path's arithmetic on the CPU: 16-bit operands, fp32 accumulate.
 
     Rounding points (cf. conv.hip / transformer.hip): the normalised input;
@@ -149,7 +171,10 @@ def forward_emulated(sd, img: torch.Tensor, pos_index=None, dtype: str = "bf16",
     feats = []
     for i, (ci, bi) in enumerate(stem_indices()):
         w, b = fold_bn(sd, ci, bi)
-        h = F.relu(F.conv2d(h, r(w), b, padding=1))
+        if i in wino:   # conv layers (0-based) the HIP path runs as Winograd F(2,3)
+            h = F.relu(conv3x3_wino_f23(h, w, b, dtype))
+        else:
+            h = F.relu(F.conv2d(h, r(w), b, padding=1))
         if i in POOL_AFTER:
             h = F.max_pool2d(h, 2, 2)
         h = r(h)

@@ -19,6 +19,10 @@ Per Winograd layer, the kernel's arithmetic (Lavin & Gray 2016, F(2x2,3x3)):
     the direct path's output.
 Every other rounding point is the direct path's (oracle emulation).
 
+Two forms: F(2x2,3x3) (2-D, this file's winograd_conv: 4/9 of the MFMAs)
+and F(2,3) along x (oracle.cvit_torch.conv3x3_wino_f23: what wino.hip
+computes, 2/3 of the MFMAs).
+
 Test infrastructure only (imports oracle/).
 
     python tools/winograd_budget.py [--n 256] [--threads 8]
@@ -38,8 +42,8 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 from fac_fake_amd.weights import make_crops, make_state_dict  # noqa: E402
-from oracle.cvit_torch import (LN_EPS, POOL_AFTER, _pos_rows, fold_bn, forward_fp32, normalize_u8,  # noqa: E402
-                               round_to, stem_indices, to_torch_sd)
+from oracle.cvit_torch import (LN_EPS, POOL_AFTER, _pos_rows, conv3x3_wino_f23, fold_bn,  # noqa: E402
+                               forward_emulated, forward_fp32, normalize_u8, round_to, stem_indices, to_torch_sd)
 
 BT = torch.tensor([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], dtype=torch.float64)
 G = torch.tensor([[1, 0, 0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0, 0, 1]], dtype=torch.float64)
@@ -132,9 +136,14 @@ def main():
     }
     for dt in ("fp16", "bf16"):
         for name, s in sets.items():
-            v = dp(forward(sd, img, pos, dt, s, dt), ref)
-            rows[f"{dt}: {name}"] = v
-            print(f"{dt}  {name:28s} max|dp| {v:.3e}", flush=True)
+            # F(2,3) along x: what conv3x3_wino (wino.hip) computes, via the oracle's emulation
+            v = dp(forward_emulated(sd, img, pos, dt, wino=s), ref)
+            rows[f"{dt}: F(2,3) x: {name}"] = v
+            print(f"{dt}  F(2,3) along x   {name:28s} max|dp| {v:.3e}", flush=True)
+            if s:
+                v = dp(forward(sd, img, pos, dt, s, dt), ref)
+                rows[f"{dt}: F(2x2,3x3): {name}"] = v
+                print(f"{dt}  F(2x2,3x3)       {name:28s} max|dp| {v:.3e}", flush=True)
     if args.out:
         Path(args.out).write_text(json.dumps({"n_crops": args.n, "vs": "fp32 reference forward (oracle)",
                                               "bar": 1e-3, "max_abs_dprob": rows}, indent=1) + "\n")
