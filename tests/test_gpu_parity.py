@@ -836,7 +836,7 @@ def test_wino_forward_vs_emulation_and_goldens(models, golden, dt, torch_threads
     whole forward against the oracle's emulation with the same layers as
     Winograd, and, at fp16, the reference's fp32 goldens within the 1e-3
     per-frame bar (tools/winograd_budget.py holds the budget)."""
-    from oracle.cvit_torch import forward_emulated, normalize_u8
+    from oracle.cvit_torch import forward_emulated, forward_fp32, normalize_u8
     from fac_fake_amd.weights import make_state_dict
     m = models[dt]
     g256 = golden("golden_b256.npz")
@@ -850,6 +850,11 @@ def test_wino_forward_vs_emulation_and_goldens(models, golden, dt, torch_threads
     err = np.abs(_sig(lg.astype(np.float64)) - _sig(g256["logits"].astype(np.float64))).max()
     if dt == "fp16":
         assert err <= 1e-3, err
-    emu = forward_emulated(make_state_dict(0), normalize_u8(c4), np.arange(4), dt,
-                           wino=set(range(6, 17))).numpy()
-    assert np.abs(_sig(lg4) - _sig(emu)).max() <= (2e-4 if dt == "fp16" else 2e-3)
+    # the distance from fp32 is what the Winograd rounding points give (the
+    # emulation with the same layers as Winograd), as test_error_envelope_end_to_end
+    sd = make_state_dict(0)
+    x = normalize_u8(c4)
+    emu = forward_emulated(sd, x, np.arange(4), dt, wino=set(range(6, 17)))
+    fp = forward_fp32(sd, x, np.arange(4))
+    got = torch.from_numpy(lg4)
+    assert _rms_rel(got, fp) <= 1.6 * _rms_rel(emu, fp) + 1e-4, (_rms_rel(got, fp), _rms_rel(emu, fp))
