@@ -26,7 +26,7 @@ with the normalisation fused into conv1, and ``dtype`` ("fp16" or "bf16": the
 "fp16", the parity-grade mode (per-frame probabilities within the north
 star's 1e-3 of the fp32 reference, DESIGN.md §3.5) at the same MFMA rate;
 "bf16" -- which bench.py selects for the bf16 throughput metric -- moves
-them by up to 4.0e-3 on config 2's 256 golden crops (measured, BENCH_r03;
+them by up to 4.0e-3 on config 2's 256 golden crops (measured, BENCH_r04 and r05;
 the oracle's emulated bf16 rounding alone gives 5.3e-3 there,
 tests/golden/bf16_envelope.json) and is an explicit opt-in.
 """
