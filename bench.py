@@ -318,7 +318,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
 
 
 def resvitkan_measurement(dev, dtype: str, world: int, B: int = 256, steps: int = 10, warmup: int = 3,
-                          chunk: int | None = None):
+                          chunk: int | None = None, roofline: bool = True):
     """Config 5 (BASELINE.json configs[4]): ResVitKan forward (ResNet-50 stem
     + CViT encoder + KAN head, fac_fake_amd/resvitkan.py) on B synthetic
     uint8 crops resident in HBM, slot j mod 32, one hipGraph per step;
@@ -357,9 +357,12 @@ def resvitkan_measurement(dev, dtype: str, world: int, B: int = 256, steps: int 
     v = world * B * steps / el
     peak = PEAK_TFLOPS[dtype]
     assert torch.isfinite(out).all()
+    ms = el / steps * 1e3
+    if not roofline:
+        return {"workload": f"ResVitKan forward, B={B} crops per GPU", "value": round(v, 1), "unit": "face-crops/s",
+                "ms_per_step": round(ms, 3)}
     with torch.cuda.stream(s):
         lr = layer_roofline_ms(lambda: m.forward_u8(crops, pos_index=pidx), dtype)
-    ms = el / steps * 1e3
     lr["fraction_of_step"] = round(lr["roofline_ms"] / ms, 4)
     return {"workload": f"config 5: ResVitKan forward (ResNet-50 + CViT encoder + KAN head), B={B} crops per GPU, "
                         "hipGraph per step", "value": round(v, 1), "unit": "face-crops/s", "n_gpus": world,
@@ -372,9 +375,11 @@ def resvitkan_measurement(dev, dtype: str, world: int, B: int = 256, steps: int 
 S3D_FLOP_PER_CLIP = 8.95e9   # per 16x112x112 clip (Conv3d hooks over S3D/model.py)
 
 
-def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, warmup: int = 3, srm: str = "no"):
+def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, warmup: int = 3, srm: str = "no",
+                    u8: bool = True, roofline: bool = True):
     """Config 4 (BASELINE.json configs[3]): S3D forward (fac_fake_amd/s3d.py) on
-    B synthetic raw 16x112x112 clips resident in HBM, one hipGraph per step;
+    B synthetic raw 16x112x112 clips resident in HBM (uint8 decoded frames,
+    or with u8=False the reference's float clip), one hipGraph per step;
     independent per rank (weak scaling), clips/s summed over ranks."""
     from fac_fake_amd.s3d import S3D
     from fac_fake_amd.weights import make_s3d_state_dict, s3d_clips
@@ -382,7 +387,8 @@ def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, w
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, srm == "yes").items()})
     # the clips as decoded frames (uint8: S3D-test.py:94-96's values before its
     # float cast, bit-identical logits to the fp32 clip, a quarter of the bytes)
-    x = torch.from_numpy(s3d_clips(B, 16, 112, seed=50 + int(os.environ.get("RANK", "0")))).to(torch.uint8).to(dev)
+    x = torch.from_numpy(s3d_clips(B, 16, 112, seed=50 + int(os.environ.get("RANK", "0"))))
+    x = (x.to(torch.uint8) if u8 else x.float()).to(dev)
     s = torch.cuda.Stream(dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
@@ -407,9 +413,12 @@ def s3d_measurement(dev, dtype: str, world: int, B: int = 64, steps: int = 10, w
         el = float(t.item())
     v = world * B * steps / el
     assert torch.isfinite(out).all()
+    ms = el / steps * 1e3
+    if not roofline:
+        return {"workload": f"S3D forward, B={B} raw {'uint8' if u8 else 'fp32'} 16x112x112 clips per GPU",
+                "value": round(v, 1), "unit": "clips/s", "ms_per_step": round(ms, 3)}
     with torch.cuda.stream(s):
         lr = layer_roofline_ms(lambda: m(x), dtype)
-    ms = el / steps * 1e3
     lr["fraction_of_step"] = round(lr["roofline_ms"] / ms, 4)
     return {"workload": f"config 4: S3D forward (SRM_net={srm}), B={B} raw uint8 16x112x112 clips per GPU, "
                         "hipGraph per step",
@@ -696,8 +705,15 @@ def main():
         del model
     if not args.no_s3d:
         line["config4"] = s3d_measurement(dev, args.dtype, world, B=args.s3d_batch)
+        # the round-3 workload (384 fp32 clips per GPU), so the
+        # trend compares like with like (the batch and the uint8 clips moved
+        # the headline config-4 number by ~15 % in round 4)
+        line["config4"]["round3_workload"] = s3d_measurement(dev, args.dtype, world, B=384, u8=False, steps=5,
+                                                             warmup=2, roofline=False)
     if not args.no_resvitkan:
         line["config5"] = resvitkan_measurement(dev, args.dtype, world, args.rvk_batch)
+        line["config5"]["round3_workload"] = resvitkan_measurement(dev, args.dtype, world, 1024, steps=5, warmup=2,
+                                                                   roofline=False)
     if not args.no_repbn8:
         line["variant_repbn8"] = repbn8_measurement(dev, args.dtype, world)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

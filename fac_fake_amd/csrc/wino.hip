@@ -36,10 +36,24 @@
 namespace fac {
 
 // V = a + b (S > 0) or a - b (S < 0) on 8 16-bit values, rounded once.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <int S>
 __device__ __forceinline__ u16x8 wino_combine(F16, u16x8 a, u16x8 b) {
-  const f16x8 x = __builtin_bit_cast(f16x8, a), y = __builtin_bit_cast(f16x8, b);
-  return __builtin_bit_cast(u16x8, S > 0 ? x + y : x - y);  // 4 v_pk_add_f16
+  // two-wide pieces, so the backend emits one v_pk_add_f16 (neg modifier for
+  // the difference) per pair; on the 8-wide vector it scalarised to
+  // v_sub_f16 + v_sub_f16_sdwa + v_pack_b32_f16 per pair
+  // (the difference as an explicit v_pk_add_f16 with negated second operand:
+  // written in C, the f16x2 subtraction was scalarised too)
+  const u32x4 x = __builtin_bit_cast(u32x4, a), y = __builtin_bit_cast(u32x4, b);
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (S > 0)
+      asm("v_pk_add_f16 %0, %1, %2" : "=v"(r[i]) : "v"(x[i]), "v"(y[i]));
+    else
+      asm("v_pk_add_f16 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r[i]) : "v"(x[i]), "v"(y[i]));
+  }
+  return __builtin_bit_cast(u16x8, r);
 }
 template <int S>
 __device__ __forceinline__ u16x8 wino_combine(BF16, u16x8 a, u16x8 b) {
