@@ -72,6 +72,26 @@ def reference_mask_poisons(mask, B: int, heads: int = 8, n_tokens: int = 2) -> b
 _SLOTS: dict = {}
 
 
+def weight_versions(module: nn.Module) -> tuple:
+    """(version counter, data pointer) of every parameter and buffer of a
+    drop-in's fixed container tree: the weights are re-uploaded when an
+    in-place update or a swapped tensor changes this.  The (module, name)
+    slots are listed once; walking them costs ~40-70 us per call, against
+    ~0.5 ms for the state_dict() this replaced (it ran on every forward, the
+    reference's one-video call included)."""
+    slots = module.__dict__.get("_wv_slots")
+    if slots is None:
+        slots = [(m._parameters, k) for _, m in module.named_modules() for k in m._parameters] + \
+                [(m._buffers, k) for _, m in module.named_modules() for k in m._buffers]
+        module.__dict__["_wv_slots"] = slots
+    out = []
+    for d, k in slots:
+        t = d[k]
+        out.append(t._version)
+        out.append(t.data_ptr())
+    return tuple(out)
+
+
 def _default_slots(device) -> torch.Tensor:
     """int32 arange(32) on `device`, made once: the default slots 0..B-1 of a
     B <= 32 call (cvit.py:175) as a slice, with no per-call launch or copy."""
@@ -145,8 +165,7 @@ class CViT(nn.Module):
 
     # ------------------------------------------------------------------ weights
     def _versions(self):
-        return tuple(t._version for t in self.state_dict(keep_vars=True).values()) + (
-            tuple(t.data_ptr() for t in self.parameters()),)
+        return weight_versions(self)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)

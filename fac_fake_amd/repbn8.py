@@ -38,7 +38,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .cvit import MAX_SLOTS, _Node, reference_mask_poisons
+from .cvit import MAX_SLOTS, _Node, reference_mask_poisons, weight_versions
 from .ops import TORCH16, fold_bn, sigmoid
 from .weights import REPBN8_LAYERS, repbn8_param_specs
 
@@ -129,8 +129,7 @@ class CViT(nn.Module):
 
     # ------------------------------------------------------------------ weights
     def _versions(self):
-        return tuple(t._version for t in self.state_dict(keep_vars=True).values()) + (
-            tuple(t.data_ptr() for t in self.parameters()),)
+        return weight_versions(self)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)

@@ -33,7 +33,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .cvit import MAX_SLOTS, _Node, reference_mask_poisons
+from .cvit import MAX_SLOTS, _Node, reference_mask_poisons, weight_versions
 from .ops import (TORCH16, ConvLayer, KANLinearLayer, bottleneck_pw2, conv_dual, fold_bn, pack_input_s2d,
                   pool, s2d_weight, sigmoid)
 from .weights import kan_grid, resnet50_blocks, resvitkan_param_specs
@@ -97,8 +97,7 @@ class ResVitKan(nn.Module):
 
     # ------------------------------------------------------------------ weights
     def _versions(self):
-        return tuple(t._version for t in self.state_dict(keep_vars=True).values()) + (
-            tuple(t.data_ptr() for t in self.parameters()),)
+        return weight_versions(self)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)

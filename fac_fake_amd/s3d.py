@@ -27,7 +27,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .cvit import _Node
+from .cvit import _Node, weight_versions
 from . import ops
 from .ops import TORCH16, ConvLayer, conv_split, fold_bn, max_pool_sep, pack_input, pack_input_s2d, pool, s2d_weight, sigmoid
 from .weights import s3d_base, s3d_param_specs
@@ -80,8 +80,7 @@ class S3D(nn.Module):
         self.eval()
 
     def _versions(self):
-        return tuple(t._version for t in self.state_dict(keep_vars=True).values()) + (
-            tuple(t.data_ptr() for t in self.parameters()),)
+        return weight_versions(self)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         out = super().load_state_dict(state_dict, strict=strict, assign=assign)
