@@ -3,10 +3,10 @@
 # DTYPE=fp16): rocprofv3 kernel trace + stats, then one rocprofv3 run per PMC
 # pass (MI355X_MICROARCH.md: counters are not split over passes; FETCH_SIZE and
 # WRITE_SIZE do not fit one TCC pass).  Summarise with
-#   python tools/rocprof_summary.py gpurun_out/prof_r04 profiles/r04_bf16
+#   python tools/rocprof_summary.py gpurun_out/prof_r05 profiles/r05_bf16
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 DT=${DTYPE:-bf16}
-OUT=$R/gpurun_out/prof_r04${PROF_TAG}
+OUT=$R/gpurun_out/prof_r05${PROF_TAG}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp

@@ -97,7 +97,7 @@ def stage_durations(trace_csv: Path):
         if "stem224_fused" in name:
             acc["conv1"].append(dur)
             k = 0
-        elif ("conv3x3_bn_relu" in name or "conv3x3_db" in name) and k is not None:
+        elif ("conv3x3_bn_relu" in name or "conv3x3_db" in name or "conv3x3_wino" in name) and k is not None:
             acc[f"conv{k + 4}"].append(dur)
             k += 1
         elif "gemm_nt" in name:
@@ -117,7 +117,7 @@ def per_stage(csv_path: Path, counter: str):
         if "stem224_fused" in name:
             acc["conv1"].append(float(r["Counter_Value"]))
             k = 0
-        elif ("conv3x3_bn_relu" in name or "conv3x3_db" in name) and k is not None:
+        elif ("conv3x3_bn_relu" in name or "conv3x3_db" in name or "conv3x3_wino" in name) and k is not None:
             acc[f"conv{k + 4}"].append(float(r["Counter_Value"]))
             k += 1
         elif "gemm_nt" in name:
