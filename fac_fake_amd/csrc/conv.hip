@@ -121,13 +121,20 @@ __device__ __forceinline__ void stage_tile(const f32x4 (&acc)[RTW][CTW], uint16_
 // 1: it is loaded between chunks, exposed, which halves the halo LDS so that
 // OCC = 3 workgroups share a CU and hide each other's exposed loads — the
 // 112^2 layers, whose 1-2 chunks leave little to pipeline within a box).
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true>
+// PERSIST: a workgroup walks several boxes (box blockIdx.x-derived, then
+// strided), so the per-box setup -- halo map, fragment offsets, the
+// accumulator init -- is paid once per workgroup instead of once per box
+// (the 1-2-chunk 112^2 layers spent ~380 of their ~680 VALU instructions per
+// box there, against 144 MFMAs per wave: round 5); nbox = boxes of the whole
+// launch (blockIdx.y still selects the column block).
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
+          bool PERSIST = false>
 __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
                                                        int Cin, int Cout, const uint16_t* __restrict__ zero16,
-                                                       int do_relu) {
+                                                       int do_relu, int nbox) {
   constexpr int CK = CONV_CK;
   constexpr int HH = TH + 2, HWD = TW + 2;
   constexpr int HALO_RP = halo_rp<TW>();
@@ -176,23 +183,25 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // (blockIdx % 8), so give XCD k a contiguous range of boxes; neighbouring
   // boxes then share their halo rows in that XCD's L2 instead of each
   // re-reading them from HBM (measured: the 112^2 layers fetched the full
-  // 1.27x halo overhead with the plain order).
-  int bx = blockIdx.x;
-  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  const int b = bx / tiles_per_img;
-  const int tile = bx - b * tiles_per_img;
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int y0 = ty * TH, x0 = tx * TW;
+  // 1.27x halo overhead with the plain order).  Persistent: XCD k's
+  // workgroups walk its range together, box l + k*G8 for local index l.
   const int nb = blockIdx.y;
   const int nchunks = Cin / CK;
-  const uint16_t* in_b = in + (size_t)b * H * W * Cin;
   const uint16_t* wsrc = wpk + (size_t)nb * nchunks * 9 * WSL;
+  const bool xcd_order = (gridDim.x & 7) == 0;
+  const int g8 = gridDim.x >> 3, xcd = blockIdx.x & 7, lidx = blockIdx.x >> 3;
+  const int range = PERSIST ? (nbox + 7) / 8 : g8;
+  const int first = xcd_order ? xcd * range + lidx : (int)blockIdx.x;
+  const int last = xcd_order ? (xcd * range + range < nbox ? xcd * range + range : nbox) : nbox;
+  const int stride = xcd_order ? g8 : (int)gridDim.x;
 
-  // Halo staging map, fixed across chunks: each lane of each halo glds
-  // instruction owns one 16-byte slot of the LDS image (plane q, row hy,
-  // column hx); it copies that piece of the image, or 16 zero bytes for
-  // zero padding / pitch padding (a pointer that does not move with c).
-  int hsrc[HPW];
+  // Halo staging map: each lane of each halo glds instruction owns one
+  // 16-byte slot of the LDS image (plane q, row hy, column hx); it copies
+  // that piece of the image, or 16 zero bytes for zero padding / pitch
+  // padding (a pointer that does not move with c).  The slot geometry is
+  // box-independent (packed hy | hx << 8 | q << 16, q = 4: pitch padding);
+  // the source offsets are formed per box.
+  int hgeo[HPW];
 #pragma unroll
   for (int i = 0; i < HPW; ++i) {
     const int slot = (i * 4 + wave) * 64 + lane;
@@ -208,10 +217,11 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       hy = j / HALO_RP;
       hx = j - (j / HALO_RP) * HALO_RP;
     }
-    const int y = y0 + hy - 1, x = x0 + hx - 1;
-    hsrc[i] = -1;
-    if (q < 4 && hy < HH && hx < HWD && y >= 0 && y < H && x >= 0 && x < W) hsrc[i] = (y * W + x) * Cin + q * 8;
+    if (q > 4 || hy >= HH || hx >= HWD) q = 4;
+    hgeo[i] = hy | (hx << 8) | (q << 16);
   }
+  int hsrc[HPW];
+  const uint16_t* in_b = in;
   // (the 112x112 pooled variant spills one map entry at its 128-VGPR budget:
   // the store sits in the prologue and the reload at a chunk start, both
   // outside the counted-vmcnt steps; recomputing the map per chunk instead
@@ -255,6 +265,19 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   int bbase[CTW];
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct) bbase[ct] = ((lane >> 4) * BN + (wn * CTW + ct) * 16 + (lane & 15)) * 8;
+
+  for (int bx = first; bx < last; bx += stride) {
+  const int b = bx / tiles_per_img;
+  const int tile = bx - b * tiles_per_img;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  in_b = in + (size_t)b * H * W * Cin;
+#pragma unroll
+  for (int i = 0; i < HPW; ++i) {
+    const int hy = hgeo[i] & 255, hx = (hgeo[i] >> 8) & 255, q = hgeo[i] >> 16;
+    const int y = y0 + hy - 1, x = x0 + hx - 1;
+    hsrc[i] = (q < 4 && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) ? (y * W + x) * Cin + q * 8 : -1;
+  }
 
   f32x4 acc[RTW][CTW];
 #pragma unroll
@@ -411,6 +434,9 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
     stage_tile<T, RTW, CTW, OPS, POOL, false>(acc, ostg, bias + nb * BN, wm, wn, lane);
   __syncthreads();
   store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
+  if constexpr (PERSIST) __syncthreads();  // every wave read ostg before the next box's halo lands there
+  if constexpr (!PERSIST) break;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -735,24 +761,64 @@ int conv_block_n(int H, int cout) {
   }
 }
 
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    cached[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return cached[dev];
+}
+
+// Persistent grid for nbox boxes at `occ` workgroups per CU: 8 XCD ranges of
+// ceil(nbox/8) boxes, each walked by G8 workgroups taking equally many boxes.
+static int persist_grid(int nbox, int occ) {
+  const int range = (nbox + 7) / 8, slots = occ * cu_count() / 8;
+  if (range <= slots) return 0;  // one box per workgroup anyway
+  const int per = (range + slots - 1) / slots;
+  return 8 * ((range + per - 1) / per);
+}
+
+// Persistent boxes for the pooled 112^2 tile (conv6; option "conv_persist",
+// process-wide; A/B).  The 4-per-CU 112^2 tile (128 VGPRs) and the 56^2 tile
+// spill with the loop-carried box state, so they keep one box per workgroup.
+static int g_conv_persist = 1;
+void set_conv_persist(int v) { g_conv_persist = v; }
+
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
-// spill with it; no model pools after such a layer)
-template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true>
+// spill with it; no model pools after such a layer).  PERSIST: the persistent
+// box loop (taken when the grid is larger than OCC workgroups per CU).
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true,
+          bool PERSIST = false>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   const int nbox = B * (H / TH) * (H / TW);
-  dim3 grid(nbox, Cout / BN);
+  const int pg = PERSIST && g_conv_persist ? persist_grid(nbox, OCC) : 0;
+  dim3 grid(pg ? pg : nbox, Cout / BN);
+#define FAC_BOX(P, PS) \
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, P, HB, OCC, PB, PS><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu, nbox)
   if constexpr (POOLED) {
     if (pool) {
-      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
-          <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+      if constexpr (PERSIST) {
+        if (pg) FAC_BOX(true, true);
+        else FAC_BOX(true, false);
+      } else {
+        FAC_BOX(true, false);
+      }
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
-      <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
+  if constexpr (PERSIST) {
+    if (pg) FAC_BOX(false, true);
+    else FAC_BOX(false, false);
+  } else {
+    FAC_BOX(false, false);
+  }
+#undef FAC_BOX
   return hipSuccess;
 }
 
@@ -795,7 +861,7 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
       // the pooled tile (conv6) spills at 4 per CU (128 VGPRs): 2 per CU
       // (same box: conv4-6 0.665 -> 0.60 ms)
       if (pool)
-        launch_box<T, 16, 16, 64, 4, 1, 1, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+        launch_box<T, 16, 16, 64, 4, 1, 1, 2, false, true, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       else
         launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       break;

@@ -24,6 +24,7 @@ namespace fac {
 int conv_block_n(int H, int cout);
 void set_nd_pt_wide(int v);
 void set_gemm_small(int max_m, int variant);
+void set_conv_persist(int v);
 void set_nd_occ3(int v);
 void set_pool_roll(int v);
 void set_pool_win(int v);
@@ -893,6 +894,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     drop_graphs(c);
   }
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
+  if (k == "conv_persist") {  // process-wide: 1 (default) persistent boxes for the pooled 112^2 conv; 0: one box per workgroup
+    fac::set_conv_persist(value != 0);
+    return FAC_OK;
+  }
   if (k == "wino") {
     if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "wino must be 0..7 (bit 0: 14^2, 1: 28^2, 2: 56^2)");
     c->wino = value;
