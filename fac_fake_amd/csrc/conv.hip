@@ -786,6 +786,10 @@ static int persist_grid(int nbox, int occ) {
 // spill with the loop-carried box state, so they keep one box per workgroup.
 static int g_conv_persist = 1;
 void set_conv_persist(int v) { g_conv_persist = v; }
+// the unpooled 112^2 tile (conv4, conv5): 0 = one box per workgroup at 4 per
+// CU (default); 1 / 2 = persistent at 3 / 2 per CU (option "conv112", A/B)
+static int g_conv112 = 0;
+void set_conv112(int v) { g_conv112 = v; }
 
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
 // spill with it; no model pools after such a layer).  PERSIST: the persistent
@@ -862,6 +866,10 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
       // (same box: conv4-6 0.665 -> 0.60 ms)
       if (pool)
         launch_box<T, 16, 16, 64, 4, 1, 1, 2, false, true, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      else if (g_conv112 == 1)  // A/B arms of the unpooled tile (option "conv112")
+        launch_box<T, 16, 16, 64, 4, 1, 1, 3, false, false, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      else if (g_conv112 == 2)
+        launch_box<T, 16, 16, 64, 4, 1, 1, 2, false, false, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       else
         launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       break;
