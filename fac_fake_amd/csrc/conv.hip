@@ -117,24 +117,48 @@ __device__ __forceinline__ void stage_tile(const f32x4 (&acc)[RTW][CTW], uint16_
   }
 }
 
+#ifdef CONV_STAMPS
+// Phase timeline of conv3x3_bn_relu (tools/ubench/conv_ubench.hip): s_memtime
+// of wave w of workgroup x at stamp k (0 start, 1 prologue landed, 2..10 after
+// chunk 0's nine step barriers, 11 last chunk done, 12 staged, 13 stored)
+__device__ unsigned long long conv_st[16384][4][14];
+#define CONV_STAMP(k)                                                                         \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    unsigned long long t_;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (blockIdx.y == 0 && blockIdx.x < 16384 && lane == 0) conv_st[blockIdx.x][wave][(k)] = t_; \
+  } while (0)
+#else
+#define CONV_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 // HB: halo buffers (2: the next chunk's halo streams in during this chunk;
 // 1: it is loaded between chunks, exposed, which halves the halo LDS so that
 // OCC = 3 workgroups share a CU and hide each other's exposed loads — the
 // 112^2 layers, whose 1-2 chunks leave little to pipeline within a box).
-// PERSIST: a workgroup walks several boxes (box blockIdx.x-derived, then
-// strided), so the per-box setup -- halo map, fragment offsets, the
-// accumulator init -- is paid once per workgroup instead of once per box
-// (the 1-2-chunk 112^2 layers spent ~380 of their ~680 VALU instructions per
-// box there, against 144 MFMAs per wave: round 5); nbox = boxes of the whole
-// launch (blockIdx.y still selects the column block).
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
-          bool PERSIST = false>
+// (Round 5, measured and not kept: persistent workgroups walking several
+// boxes each, so the per-box setup -- halo map, fragment offsets -- is paid
+// once per workgroup.  Bit-identical, but slower on every 112^2 arm, same
+// box: the pooled tile at 2 per CU conv6 199 -> 246 us, the unpooled one at
+// 3 / 2 per CU conv4 161 -> 185 / 182 us and conv5 240 -> 281 / 297 us: a
+// persistent grid loses the overlap of one workgroup's exposed halo load
+// with its neighbours' MFMAs that the hardware's dispatch order gives.)
+// (Round 5, also not kept: a 9-slice weight ring for the 112^2 layers, so a
+// 1-chunk layer's whole weight block is in flight from the prologue on and
+// its 9 steps never wait on L2.  Bit-identical; 61 KB of LDS, i.e. 2 per CU:
+// conv4 161 -> 188 us, conv5 / conv6 +0-20 %.  The 3-slice ring's waits are
+// not what holds these layers back; occupancy is.)
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true>
 __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
                                                        uint16_t* __restrict__ out, int H, int W,
                                                        int Cin, int Cout, const uint16_t* __restrict__ zero16,
-                                                       int do_relu, int nbox) {
+                                                       int do_relu) {
   constexpr int CK = CONV_CK;
   constexpr int HH = TH + 2, HWD = TW + 2;
   constexpr int HALO_RP = halo_rp<TW>();
@@ -179,29 +203,28 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
+  CONV_STAMP(0);
   // XCD-aware box order: workgroups are dealt round-robin to the 8 XCDs
   // (blockIdx % 8), so give XCD k a contiguous range of boxes; neighbouring
   // boxes then share their halo rows in that XCD's L2 instead of each
   // re-reading them from HBM (measured: the 112^2 layers fetched the full
-  // 1.27x halo overhead with the plain order).  Persistent: XCD k's
-  // workgroups walk its range together, box l + k*G8 for local index l.
+  // 1.27x halo overhead with the plain order).
   const int nb = blockIdx.y;
   const int nchunks = Cin / CK;
   const uint16_t* wsrc = wpk + (size_t)nb * nchunks * 9 * WSL;
-  const bool xcd_order = (gridDim.x & 7) == 0;
-  const int g8 = gridDim.x >> 3, xcd = blockIdx.x & 7, lidx = blockIdx.x >> 3;
-  const int range = PERSIST ? (nbox + 7) / 8 : g8;
-  const int first = xcd_order ? xcd * range + lidx : (int)blockIdx.x;
-  const int last = xcd_order ? (xcd * range + range < nbox ? xcd * range + range : nbox) : nbox;
-  const int stride = xcd_order ? g8 : (int)gridDim.x;
+  int bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  const int b = bx / tiles_per_img;
+  const int tile = bx - b * tiles_per_img;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const uint16_t* const in_b = in + (size_t)b * H * W * Cin;
 
   // Halo staging map: each lane of each halo glds instruction owns one
   // 16-byte slot of the LDS image (plane q, row hy, column hx); it copies
   // that piece of the image, or 16 zero bytes for zero padding / pitch
-  // padding (a pointer that does not move with c).  The slot geometry is
-  // box-independent (packed hy | hx << 8 | q << 16, q = 4: pitch padding);
-  // the source offsets are formed per box.
-  int hgeo[HPW];
+  // padding (a pointer that does not move with c).
+  int hsrc[HPW];
 #pragma unroll
   for (int i = 0; i < HPW; ++i) {
     const int slot = (i * 4 + wave) * 64 + lane;
@@ -217,11 +240,11 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       hy = j / HALO_RP;
       hx = j - (j / HALO_RP) * HALO_RP;
     }
-    if (q > 4 || hy >= HH || hx >= HWD) q = 4;
-    hgeo[i] = hy | (hx << 8) | (q << 16);
+    const int y = y0 + hy - 1, x = x0 + hx - 1;
+    hsrc[i] = (q < 4 && hy < HH && hx < HWD && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+                  ? (y * W + x) * Cin + q * 8
+                  : -1;
   }
-  int hsrc[HPW];
-  const uint16_t* in_b = in;
   // (the 112x112 pooled variant spills one map entry at its 128-VGPR budget:
   // the store sits in the prologue and the reload at a chunk start, both
   // outside the counted-vmcnt steps; recomputing the map per chunk instead
@@ -266,19 +289,6 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct) bbase[ct] = ((lane >> 4) * BN + (wn * CTW + ct) * 16 + (lane & 15)) * 8;
 
-  for (int bx = first; bx < last; bx += stride) {
-  const int b = bx / tiles_per_img;
-  const int tile = bx - b * tiles_per_img;
-  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int y0 = ty * TH, x0 = tx * TW;
-  in_b = in + (size_t)b * H * W * Cin;
-#pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    const int hy = hgeo[i] & 255, hx = (hgeo[i] >> 8) & 255, q = hgeo[i] >> 16;
-    const int y = y0 + hy - 1, x = x0 + hx - 1;
-    hsrc[i] = (q < 4 && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) ? (y * W + x) * Cin + q * 8 : -1;
-  }
-
   f32x4 acc[RTW][CTW];
 #pragma unroll
   for (int rt = 0; rt < RTW; ++rt)
@@ -300,6 +310,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   if constexpr (PB) issue_w(2, nsteps > 2 ? wsrc + 2 * WSL : wsrc);
   issue_halo(hbase, 0);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  CONV_STAMP(1);
   // PB: the B fragments of tap t+1 are read during tap t as well (slice s+1
   // is retired one barrier earlier, slice s+3 is issued at step s into the
   // slot slice s vacated when its fragments went to registers in step s-1).
@@ -401,6 +412,9 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
 #endif
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(%1)\n\ts_barrier" ::"n"(N), "n"(L) : "memory");
       __builtin_amdgcn_sched_barrier(0);
+#ifdef CONV_STAMPS
+      if (c == 0) CONV_STAMP(2 + t);
+#endif
     };
     step(std::integral_constant<int, 0>{});
     step(std::integral_constant<int, 1>{});
@@ -413,6 +427,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
     step(std::integral_constant<int, 8>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy slices land before LDS is reused / the wave ends
+  CONV_STAMP(11);
   const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
   const int oy0 = POOL ? y0 / 2 : y0, ox0 = POOL ? x0 / 2 : x0;
   __syncthreads();
@@ -433,10 +448,12 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   else
     stage_tile<T, RTW, CTW, OPS, POOL, false>(acc, ostg, bias + nb * BN, wm, wn, lane);
   __syncthreads();
+  CONV_STAMP(12);
   store_tile<TH, TW, BN, POOL>(ostg, out, b, Ho, Wo, oy0, ox0, Cout, nb * BN, tid);
-  if constexpr (PERSIST) __syncthreads();  // every wave read ostg before the next box's halo lands there
-  if constexpr (!PERSIST) break;
-  }
+#ifdef CONV_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  CONV_STAMP(13);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -761,68 +778,23 @@ int conv_block_n(int H, int cout) {
   }
 }
 
-static int cu_count() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int n = 0;
-    cached[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
-  }
-  return cached[dev];
-}
-
-// Persistent grid for nbox boxes at `occ` workgroups per CU: 8 XCD ranges of
-// ceil(nbox/8) boxes, each walked by G8 workgroups taking equally many boxes.
-static int persist_grid(int nbox, int occ) {
-  const int range = (nbox + 7) / 8, slots = occ * cu_count() / 8;
-  if (range <= slots) return 0;  // one box per workgroup anyway
-  const int per = (range + slots - 1) / slots;
-  return 8 * ((range + per - 1) / per);
-}
-
-// Persistent boxes for the pooled 112^2 tile (conv6; option "conv_persist",
-// process-wide; A/B).  The 4-per-CU 112^2 tile (128 VGPRs) and the 56^2 tile
-// spill with the loop-carried box state, so they keep one box per workgroup.
-static int g_conv_persist = 1;
-void set_conv_persist(int v) { g_conv_persist = v; }
-// the unpooled 112^2 tile (conv4, conv5): 0 = one box per workgroup at 4 per
-// CU (default); 1 / 2 = persistent at 3 / 2 per CU (option "conv112", A/B)
-static int g_conv112 = 0;
-void set_conv112(int v) { g_conv112 = v; }
-
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
-// spill with it; no model pools after such a layer).  PERSIST: the persistent
-// box loop (taken when the grid is larger than OCC workgroups per CU).
-template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true,
-          bool PERSIST = false>
+// spill with it; no model pools after such a layer).
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
-  const int nbox = B * (H / TH) * (H / TW);
-  const int pg = PERSIST && g_conv_persist ? persist_grid(nbox, OCC) : 0;
-  dim3 grid(pg ? pg : nbox, Cout / BN);
-#define FAC_BOX(P, PS) \
-  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, P, HB, OCC, PB, PS><<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu, nbox)
+  dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if constexpr (POOLED) {
     if (pool) {
-      if constexpr (PERSIST) {
-        if (pg) FAC_BOX(true, true);
-        else FAC_BOX(true, false);
-      } else {
-        FAC_BOX(true, false);
-      }
+      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
+          <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  if constexpr (PERSIST) {
-    if (pg) FAC_BOX(false, true);
-    else FAC_BOX(false, false);
-  } else {
-    FAC_BOX(false, false);
-  }
-#undef FAC_BOX
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
+      <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
 
@@ -865,11 +837,7 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
       // the pooled tile (conv6) spills at 4 per CU (128 VGPRs): 2 per CU
       // (same box: conv4-6 0.665 -> 0.60 ms)
       if (pool)
-        launch_box<T, 16, 16, 64, 4, 1, 1, 2, false, true, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      else if (g_conv112 == 1)  // A/B arms of the unpooled tile (option "conv112")
-        launch_box<T, 16, 16, 64, 4, 1, 1, 3, false, false, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      else if (g_conv112 == 2)
-        launch_box<T, 16, 16, 64, 4, 1, 1, 2, false, false, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+        launch_box<T, 16, 16, 64, 4, 1, 1, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       else
         launch_box<T, 16, 16, 64, 4, 1, 1, 4, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       break;

@@ -24,8 +24,6 @@ namespace fac {
 int conv_block_n(int H, int cout);
 void set_nd_pt_wide(int v);
 void set_gemm_small(int max_m, int variant);
-void set_conv_persist(int v);
-void set_conv112(int v);
 void set_nd_occ3(int v);
 void set_pool_roll(int v);
 void set_pool_win(int v);
@@ -895,15 +893,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     drop_graphs(c);
   }
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
-  if (k == "conv_persist") {  // process-wide: 1 (default) persistent boxes for the pooled 112^2 conv; 0: one box per workgroup
-    fac::set_conv_persist(value != 0);
-    return FAC_OK;
-  }
-  if (k == "conv112") {  // process-wide A/B: the unpooled 112^2 conv tile (0 default, 1 / 2 persistent at 3 / 2 per CU)
-    if (value < 0 || value > 2) return set_err(c, FAC_ERR_ARG, "conv112 must be 0..2");
-    fac::set_conv112(value);
-    return FAC_OK;
-  }
   if (k == "wino") {
     if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "wino must be 0..7 (bit 0: 14^2, 1: 28^2, 2: 56^2)");
     c->wino = value;

@@ -858,28 +858,3 @@ def test_wino_forward_vs_emulation_and_goldens(models, golden, dt, torch_threads
     fp = forward_fp32(sd, x, np.arange(4))
     got = torch.from_numpy(lg4)
     assert _rms_rel(got, fp) <= 1.6 * _rms_rel(emu, fp) + 1e-4, (_rms_rel(got, fp), _rms_rel(emu, fp))
-
-
-@pytest.mark.parametrize("B", [37, 256])
-def test_persistent_conv_boxes_are_bit_identical(models, B):
-    """The pooled 112^2 conv (conv6) walks its boxes persistently (option
-    conv_persist, the default): conv6's pooled output and the logits are
-    bit-identical to one box per workgroup, for a batch whose boxes do not
-    divide evenly over the workgroups (B = 37: 1813 boxes) and config 2's."""
-    from fac_fake_amd import _lib
-    lib = _lib.load()
-    m = models["fp16"]
-    x = torch.from_numpy(make_crops(B, seed=66)).to(DEV)
-    pidx = (torch.arange(B) % 32).to(torch.int32)
-    outs = {}
-    try:
-        for v in (1, 0):
-            m.set_option("conv_persist", v)
-            c6 = torch.empty(B, 56, 56, 64, dtype=torch.float16, device=DEV)
-            _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), B, 5, c6.data_ptr(), None), m._ctx, "dbg")
-            lg = m.forward_u8(x, pos_index=pidx)
-            torch.cuda.synchronize()
-            outs[v] = (c6.view(torch.int16).cpu(), lg.cpu())
-    finally:
-        m.set_option("conv_persist", 1)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
