@@ -62,7 +62,10 @@ __device__ __forceinline__ void box_pixel(int m, int& py, int& px) {
 }
 
 // Stage an OPIX x BN tile (row stride OPS, window-major rows) from LDS to
-// NHWC global memory with 16-byte stores in raster order.
+// NHWC global memory with 16-byte stores in raster order.  (Round 5, not
+// kept: write-through `sc1` stores, which drop the line from the XCD's L2,
+// so the output stream would not evict the halo rows neighbouring boxes
+// re-read: conv4-17 within noise, same box.)
 template <int TH, int TW, int BN, bool POOL>
 __device__ __forceinline__ void store_tile(const uint16_t* ostg, uint16_t* out, int b, int Ho, int Wo,
                                            int oy0, int ox0, int Cout, int n0, int tid) {
@@ -147,12 +150,15 @@ __device__ unsigned long long conv_st[16384][4][14];
 // 3 / 2 per CU conv4 161 -> 185 / 182 us and conv5 240 -> 281 / 297 us: a
 // persistent grid loses the overlap of one workgroup's exposed halo load
 // with its neighbours' MFMAs that the hardware's dispatch order gives.)
-// (Round 5, also not kept: a 9-slice weight ring for the 112^2 layers, so a
-// 1-chunk layer's whole weight block is in flight from the prologue on and
-// its 9 steps never wait on L2.  Bit-identical; 61 KB of LDS, i.e. 2 per CU:
-// conv4 161 -> 188 us, conv5 / conv6 +0-20 %.  The 3-slice ring's waits are
-// not what holds these layers back; occupancy is.)
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true>
+// WR: weight-ring depth in tap slices, 3 or 9.  9 (no PB): slice s+8 is
+// issued at step s, so each slice has eight steps to land instead of two --
+// for grids of about one workgroup per CU (few crops), where no co-resident
+// workgroup covers a step's wait on L2 (past the end: dummy re-reads of
+// slice 0 into dead slots, as with 3).  (Round 5: the 9-slice ring for the 112^2 layers, 61 KB of LDS,
+// i.e. 2 per CU instead of 4, was slower, conv4 161 -> 188 us: there
+// occupancy, not the slice wait, sets the rate.)
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
+          int WR = 3>
 __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
@@ -190,7 +196,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   constexpr int WSL = BN * CK;              // elements per tap slice
   constexpr int OPIX = POOL ? NPIX / 4 : NPIX;
   constexpr int OPS = BN + 8;
-  constexpr int OPER = HB * HALO + 3 * WSL;   // halo buffer(s) + 3-slot weight ring
+  constexpr int OPER = HB * HALO + WR * WSL;  // halo buffer(s) + WR-slot weight ring
+  static_assert(WR == 3 || WR == 9, "weight ring: 3 or 9 slices");
   constexpr int OSTG = (POOL ? RT * 4 : RT * 16) * OPS;  // padded: epilogue writes unguarded
   constexpr int SMEM = OPER > OSTG ? OPER : OSTG;
   static_assert(WM * WN == 4, "4 waves");
@@ -305,9 +312,14 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // barriers": counted vmcnt + raw s_barrier, never __syncthreads here).
   // The next chunk's halo is fetched at t = 0 and written at t = 8.
   const int nsteps = nchunks * 9;
-  issue_w(0, wsrc);
-  issue_w(1, wsrc + WSL);
-  if constexpr (PB) issue_w(2, nsteps > 2 ? wsrc + 2 * WSL : wsrc);
+  if constexpr (WR == 9) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) issue_w(k, k < nsteps ? wsrc + k * WSL : wsrc);
+  } else {
+    issue_w(0, wsrc);
+    issue_w(1, wsrc + WSL);
+    if constexpr (PB) issue_w(2, nsteps > 2 ? wsrc + 2 * WSL : wsrc);
+  }
   issue_halo(hbase, 0);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   CONV_STAMP(1);
@@ -343,31 +355,39 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
     const uint16_t* hb = hbase + (HB == 2 ? (c & 1) * HALO : 0);
     const uint16_t* hbn = hbase + (HB == 2 ? ((c + 1) & 1) * HALO : 0);
     const bool next_h = c + 1 < nchunks;
-    const uint16_t* wnext = wsrc + (size_t)(c * 9 + 2) * WSL;
+    const uint16_t* wnext = wsrc + (size_t)(c * 9 + WR - 1) * WSL;
     auto step = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
+      // WR = 9: the next chunk's halo goes out first at t = 0, ahead of slice
+      // 9c+8, so the step-7 wait (which retires slice 9c+8) retires it too,
+      // before step 8 reads it
+      if (WR == 9 && HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
       // slice s+2 (past the end: a dummy re-read of slice 0 into a dead slot)
       // issue order: slice s+2, then (t = 0) the next chunk's halo into the
       // other halo buffer (on the last chunk a dummy re-read of this chunk);
       // glds are LDS writes, so the compiler keeps them in program order
-      if constexpr (PB)
+      // (WR = 9: slice s+8 into the slot of slice s-1, read in step s-1, or
+      // with PB in step s-2)
+      if constexpr (WR == 9)
+        issue_w((t + 8) % 9, (c * 9 + t + 8 < nsteps) ? wnext + t * WSL : wsrc);
+      else if constexpr (PB)
         issue_w(t % 3, (c * 9 + t + 3 < nsteps) ? wnext + (t + 1) * WSL : wsrc);
       else
         issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
-      if (HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
+      if (WR == 3 && HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
       u16x8 bfr[CTW], bnx[CTW];
       if constexpr (PB) {
 #pragma unroll
         for (int ct = 0; ct < CTW; ++ct) bfr[ct] = bcur[ct];
       } else {
-        const uint16_t* wb = wring + (t % 3) * WSL;
+        const uint16_t* wb = wring + (t % WR) * WSL;
 #pragma unroll
         for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
       }
       constexpr int kyn = t < 8 ? (t + 1) / 3 : 0, kxn = t < 8 ? (t + 1) % 3 : 0;
       constexpr int ntoff = PM ? (kyn * RPX + kxn) * 32 : (kyn * HALO_RP + kxn) * 8;
       const uint16_t* hnx = t < 8 ? hb : hbn;
-      const uint16_t* wbn = wring + ((t + 1) % 3) * WSL;
+      const uint16_t* wbn = wring + ((t + 1) % WR) * WSL;
 #pragma unroll
       for (int rt = 0; rt < RTW; ++rt) {
 #pragma unroll
@@ -399,7 +419,11 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
       // step refills) and leaves the youngest ones, the A-fragment prefetches
       // for the next tap (halo buffers, not rewritten here), in flight: L of
       // them (with PB, A(0) sits in one group with the bnx reads).
-      constexpr int N = WPW + (HB == 2 && t <= 1 ? HPW : 0);
+      // (WR = 9: slices s+2 .. s+8 and the next halo while t <= 6; with PB,
+      // whose next step reads slice s+2, slices s+3 .. s+8 and the halo
+      // while t <= 5)
+      constexpr int N = WR == 3 ? WPW + (HB == 2 && t <= 1 ? HPW : 0)
+                                : (PB ? 6 * WPW + (HB == 2 && t <= 5 ? HPW : 0) : 7 * WPW + (HB == 2 && t <= 6 ? HPW : 0));
       // The relaxed wait relies on the issue order; fac_fake_amd/isa_check.py
       // verifies it on the built code object (each of the L youngest LDS ops
       // before every such barrier is a ds_read_b128 whose registers next feed
@@ -479,7 +503,10 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
 // be an inline-asm output either: the compiler takes such a value as written
 // at the asm and may reuse its registers -- a dummy load's, once dead --
 // before the data lands; a first version faulted that way.)
-template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int OCC = 2>
+// BR: depth of the register B ring in tap slices, 3 or 9 (9: each fragment
+// is fetched eight steps ahead -- the few-crop grids, where no co-resident
+// workgroup covers a step's wait on L2; 9 x CTW x 4 VGPRs).
+template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int OCC = 2, int BR = 3>
 __global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias, uint16_t* __restrict__ out,
@@ -573,10 +600,11 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restric
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = (f32x4)0.f;
 
-  u16x8 bq[3][CTW];
+  static_assert(BR == 3 || BR == 9, "B ring: 3 or 9 slices");
+  u16x8 bq[BR][CTW];
   load_halo(0);
-  load_b(bq[0], 0);
-  load_b(bq[1], 1);
+#pragma unroll
+  for (int k = 0; k < BR - 1; ++k) load_b(bq[k], k);
   store_halo(smem);
   __syncthreads();
   u16x8 fa[RTW];
@@ -596,7 +624,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restric
     const int s0 = c * 9;
     auto step = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      load_b(bq[(t + 2) % 3], s0 + t + 2);
+      load_b(bq[(t + BR - 1) % BR], s0 + t + BR - 1);
       if constexpr (t == 0) load_halo(c + 1 < nchunks ? c + 1 : c);
       constexpr int kyn = t < 8 ? (t + 1) / 3 : 0, kxn = t < 8 ? (t + 1) % 3 : 0;
       constexpr int ntoff = (kyn * RPX + kxn) * 32;
@@ -604,7 +632,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_db(const uint16_t* __restric
 #pragma unroll
       for (int rt = 0; rt < RTW; ++rt) {
 #pragma unroll
-        for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bq[t % 3][ct], acc[rt][ct]);
+        for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bq[t % BR][ct], acc[rt][ct]);
         fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
       }
       __builtin_amdgcn_sched_group_barrier(0x020, CTW + (t == 0 ? HPW : 0), 0);
@@ -780,34 +808,35 @@ int conv_block_n(int H, int cout) {
 
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
 // spill with it; no model pools after such a layer).
-template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true>
+template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true,
+          int WR = 3>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if constexpr (POOLED) {
     if (pool) {
-      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB>
+      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, WR>
           <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB>
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, WR>
       <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
 
 // conv3x3_db launch (weights straight to VGPRs, one barrier per chunk)
-template <class T, int TH, int TW, int BN, int WM, int WN, int OCC = 2>
+template <class T, int TH, int TW, int BN, int WM, int WN, int OCC = 2, int BR = 3>
 static hipError_t launch_db(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                             int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if (pool)
-    conv3x3_db<T, TH, TW, BN, WM, WN, true, OCC>
+    conv3x3_db<T, TH, TW, BN, WM, WN, true, OCC, BR>
         <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   else
-    conv3x3_db<T, TH, TW, BN, WM, WN, false, OCC>
+    conv3x3_db<T, TH, TW, BN, WM, WN, false, OCC, BR>
         <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
@@ -822,6 +851,24 @@ static hipError_t launch_db(const uint16_t* in, const uint16_t* wpk, const float
 // rows), at 112^2 15-20 % slower (four waves re-read the same B): those keep
 // the LDS weight ring.
 
+// 9-slice weight rings for grids of at most two workgroups per CU (few crops;
+// option "conv_ring9", process-wide, A/B): bit 0 = the 14x14 / BN 64 tile
+// (the few-crop 14^2 convs, conv_small), bit 1 = it with the B-fragment
+// prefetch (PB) too, bit 2 = conv3x3_db's 4x28 / BN 128 tile (the few-crop
+// 28^2 convs)
+static int g_ring9 = 6;
+void set_conv_ring9(int v) { g_ring9 = v; }
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    cached[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return cached[dev];
+}
+
 template <class T>
 static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                                 int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* z, hipStream_t st,
@@ -829,6 +876,8 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
   if (W != H) return hipErrorInvalidValue;
   if (bn == 0) bn = conv_block_n(H, Cout);
   if (bn <= 0 || Cout % bn) return hipErrorInvalidValue;
+  const bool few = g_ring9 && (long)B * (Cout / bn) * (H == 14 ? 1 : H == 28 ? 7 : 1 << 30) <= 2L * cu_count();
+  const int ring9 = few ? g_ring9 : 0;
   switch (H * 1000 + bn) {
     case 224032: launch_box<T, 16, 16, 32, 4, 1, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     // 112: one halo buffer, 4 workgroups per CU (A/B in one process, MI355X:
@@ -845,14 +894,26 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
     case 56064: launch_box<T, 8, 28, 64, 2, 2>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28256: launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28192: launch_db<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-    case 28128: launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 28128:
+      if (ring9 & 4)
+        launch_db<T, 4, 28, 128, 1, 4, 2, 9>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      else
+        launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      break;
     // (a two-box 14x14 workgroup needs 256+ VGPRs and spills: not built)
     case 14128: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 14192:
       if (launch_box<T, 14, 14, 192, 1, 4, 2, 2, false, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
         return hipErrorInvalidValue;
       break;
-    case 14064: launch_box<T, 14, 14, 64, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 14064:
+      if (ring9 & 2)
+        launch_box<T, 14, 14, 64, 1, 4, 2, 2, true, true, 9>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      else if (ring9 & 1)
+        launch_box<T, 14, 14, 64, 1, 4, 2, 2, false, true, 9>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      else
+        launch_box<T, 14, 14, 64, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

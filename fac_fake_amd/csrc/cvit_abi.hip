@@ -21,6 +21,7 @@
 #include "common.hpp"
 
 namespace fac {
+void set_conv_ring9(int v);
 int conv_block_n(int H, int cout);
 void set_nd_pt_wide(int v);
 void set_gemm_small(int max_m, int variant);
@@ -53,6 +54,8 @@ hipError_t launch_resid_layernorm(int dtype, float* x, const float* slab, int S,
 hipError_t launch_resid_cls(int dtype, const float* x, const float* slab, int S, const float* bias, uint16_t* c, int B,
                             hipStream_t st);
 hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, float scale, hipStream_t st);
+hipError_t launch_attn_out(int dtype, const float* qkv, const uint16_t* w_out, float* slab, int B, float scale,
+                           int splits, hipStream_t st);
 hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, float* logits, float* probs, int B,
                            hipStream_t st);
 hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st);
@@ -190,9 +193,27 @@ struct fac_ctx {
   struct SmallGraph {
     int B, kind;  // kind: bit 0 = uint8 NHWC input, bit 1 = probs wanted
     hipGraphExec_t exec;
+    // direct graphs: captured on the caller's own buffers (no copies in or
+    // out); nullptr in = the copy graph of (B, kind), over g_in / g_out
+    const void* in = nullptr;
+    const int32_t* pidx = nullptr;
+    float *logits = nullptr, *probs = nullptr;
+    unsigned long long used = 0;
   };
+  // the previous small forward's buffers per (B, kind): a second call on the
+  // same buffers captures a direct graph for them
+  struct LastCall {
+    int B, kind;
+    const void* in;
+    const int32_t* pidx;
+    float *logits, *probs;
+  };
+  std::vector<LastCall> last_calls;
+  unsigned long long graph_clock = 0;
+  static constexpr int kDirectGraphs = 8;
   int graph_max_b = 32;
   int conv_small = 1;  // option "conv_small": 28^2 / 14^2 layers on half-width column blocks when few crops
+  int attn_fuse = 1;   // option "attn_fuse": attention + to_out in one launch for <= 32 crops
   int wino = 0;        // option "wino": bit 0 / 1 / 2 = the 14^2 / 28^2 / 56^2 layers as Winograd F(2,3)
   std::vector<SmallGraph> graphs;
   hipStream_t cap_st = nullptr;
@@ -298,6 +319,7 @@ void drop_graphs(fac_ctx* c) {
   (void)hipDeviceSynchronize();  // no replay of them is still in flight
   for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.exec);
   c->graphs.clear();
+  c->last_calls.clear();
 }
 
 int ensure_ws(fac_ctx* c, int B) {
@@ -703,6 +725,9 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
   // slabs; the following kernel (residual add + next LayerNorm, or the CLS
   // finish after the last layer) sums them in split order.
   const int SK = c->proj_splits;
+  // few rows (the reference's one-video call): attention + to_out in one
+  // launch (attn_out_gemm, bit-identical to the two)
+  const bool fuse_attn = c->attn_fuse && R <= 64 && (SK == 2 || SK == 4) && c->gemm_var[2] < 0;
   for (int l = 0; l < kDepth; ++l) {
     const TLayer& T = c->tl[l];
     if (l > 0) {
@@ -710,8 +735,13 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
     }
     HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st,
                            c->gemm_var[1]));
-    HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
-    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st, c->gemm_var[2]));
+    if (fuse_attn) {
+      HIP_TRY(c, launch_attn_out(dt, c->qkv, T.wo, c->slab, B, scale, SK, st));
+    } else {
+      HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
+      HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st,
+                             c->gemm_var[2]));
+    }
     HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, T.bo, T.ln2_g, T.ln2_b, c->xn, R, st, c->ffn_ln_eps));
     HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st,
                            c->gemm_var[3]));
@@ -746,9 +776,38 @@ int mark_done(fac_ctx* c, hipStream_t st) {
   return FAC_OK;
 }
 
-// The small-batch forward by graph replay (fac_ctx::graphs): copy the crops
-// and slots into the context's buffers, launch the graph captured for this
-// (B, kind), copy the logits (and probabilities) out.  The graph holds the
+// Capture forward_impl(in, pidx, logits, probs) at B as a graph (on the
+// context's capture stream: the captured forward must not wait on events
+// recorded outside the capture; the replay's ordering is done on the
+// caller's stream).
+int capture_forward(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
+                    hipGraphExec_t* out) {
+  if (!c->cap_st) HIP_TRY(c, hipStreamCreateWithFlags(&c->cap_st, hipStreamNonBlocking));
+  const bool tp0 = c->tail_pending[0], tp1 = c->tail_pending[1];
+  c->tail_pending[0] = c->tail_pending[1] = false;
+  HIP_TRY(c, hipStreamBeginCapture(c->cap_st, hipStreamCaptureModeThreadLocal));
+  const int rc = forward_impl(c, in, u8, B, pidx, logits, probs, c->cap_st);
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(c->cap_st, &graph);
+  c->tail_pending[0] = tp0;
+  c->tail_pending[1] = tp1;
+  if (rc != FAC_OK || ec != hipSuccess) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc != FAC_OK ? rc : set_err(c, FAC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(ec));
+  }
+  const hipError_t ei = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ei != hipSuccess) return set_err(c, FAC_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
+  return FAC_OK;
+}
+
+// The small-batch forward by graph replay (fac_ctx::graphs).  A call on the
+// same buffers (crops, slots, logits, probs) as the previous call of its
+// (B, kind) replays a graph captured on those buffers -- one graph launch,
+// nothing copied (the reference's per-video loop reuses its buffers: torch's
+// caching allocator hands the same blocks back); otherwise the crops and
+// slots are copied into the context's buffers, the (B, kind) copy graph runs
+// and the logits (and probabilities) are copied out.  Every graph holds the
 // same kernels with the same arguments as forward_impl at this B, so the
 // outputs are bit-identical to the eager forward.
 int forward_graph(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
@@ -757,6 +816,55 @@ int forward_graph(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pid
   DevGuard g(c->device);
   int rc = ensure_ws(c, B);
   if (rc) return rc;
+  const int kind = (u8 ? 1 : 0) | (probs ? 2 : 0);
+  ++c->graph_clock;
+  // direct graph for these buffers?
+  for (auto& gr : c->graphs)
+    if (gr.in && gr.B == B && gr.kind == kind && gr.in == in && gr.pidx == pidx && gr.logits == logits &&
+        gr.probs == probs) {
+      gr.used = c->graph_clock;
+      rc = order_on(c, st);
+      if (rc) return rc;
+      HIP_TRY(c, hipGraphLaunch(gr.exec, st));
+      return mark_done(c, st);
+    }
+  bool repeat = false, seen = false;
+  for (auto& lc : c->last_calls)
+    if (lc.B == B && lc.kind == kind) {
+      repeat = lc.in == in && lc.pidx == pidx && lc.logits == logits && lc.probs == probs;
+      lc = {B, kind, in, pidx, logits, probs};
+      seen = true;
+    }
+  if (!seen) c->last_calls.push_back({B, kind, in, pidx, logits, probs});
+  if (repeat) {
+    int ndirect = 0;
+    fac_ctx::SmallGraph* oldest = nullptr;
+    for (auto& gr : c->graphs)
+      if (gr.in) {
+        ++ndirect;
+        if (!oldest || gr.used < oldest->used) oldest = &gr;
+      }
+    if (ndirect >= fac_ctx::kDirectGraphs) {
+      // no replay of it may still be in flight on any stream
+      HIP_TRY(c, hipDeviceSynchronize());
+      (void)hipGraphExecDestroy(oldest->exec);
+      c->graphs.erase(c->graphs.begin() + (oldest - c->graphs.data()));
+    }
+    hipGraphExec_t ex = nullptr;
+    rc = capture_forward(c, in, u8, B, pidx, logits, probs, &ex);
+    if (rc) return rc;
+    fac_ctx::SmallGraph sg{B, kind, ex};
+    sg.in = in;
+    sg.pidx = pidx;
+    sg.logits = logits;
+    sg.probs = probs;
+    sg.used = c->graph_clock;
+    c->graphs.push_back(sg);
+    rc = order_on(c, st);
+    if (rc) return rc;
+    HIP_TRY(c, hipGraphLaunch(ex, st));
+    return mark_done(c, st);
+  }
   const size_t crop_bytes = u8 ? (size_t)kImg * kImg * 3 : (size_t)3 * kImg * kImg * 4;
   if (c->g_cap < c->graph_max_b) {
     drop_graphs(c);
@@ -781,29 +889,12 @@ int forward_graph(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pid
     return set_err(c, FAC_ERR_OOM, "graph input buffer allocation failed");
   }
   float* const g_probs = c->g_out + 2 * c->g_cap;
-  const int kind = (u8 ? 1 : 0) | (probs ? 2 : 0);
   hipGraphExec_t ex = nullptr;
   for (auto& gr : c->graphs)
-    if (gr.B == B && gr.kind == kind) ex = gr.exec;
+    if (!gr.in && gr.B == B && gr.kind == kind) ex = gr.exec;
   if (!ex) {
-    if (!c->cap_st) HIP_TRY(c, hipStreamCreateWithFlags(&c->cap_st, hipStreamNonBlocking));
-    // the captured forward must not wait on events recorded outside the
-    // capture; the replay's ordering is done on the caller's stream below
-    const bool tp0 = c->tail_pending[0], tp1 = c->tail_pending[1];
-    c->tail_pending[0] = c->tail_pending[1] = false;
-    HIP_TRY(c, hipStreamBeginCapture(c->cap_st, hipStreamCaptureModeThreadLocal));
-    rc = forward_impl(c, gin, u8, B, c->g_pidx, c->g_out, probs ? g_probs : nullptr, c->cap_st);
-    hipGraph_t graph = nullptr;
-    const hipError_t ec = hipStreamEndCapture(c->cap_st, &graph);
-    c->tail_pending[0] = tp0;
-    c->tail_pending[1] = tp1;
-    if (rc != FAC_OK || ec != hipSuccess) {
-      if (graph) (void)hipGraphDestroy(graph);
-      return rc != FAC_OK ? rc : set_err(c, FAC_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(ec));
-    }
-    const hipError_t ei = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (ei != hipSuccess) return set_err(c, FAC_ERR_HIP, std::string("graph instantiate: ") + hipGetErrorString(ei));
+    rc = capture_forward(c, gin, u8, B, c->g_pidx, c->g_out, probs ? g_probs : nullptr, &ex);
+    if (rc) return rc;
     c->graphs.push_back({B, kind, ex});
   }
   rc = order_on(c, st);
@@ -893,9 +984,19 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     drop_graphs(c);
   }
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
+  if (k == "conv_ring9") {  // process-wide A/B: 9-slice weight ring (bit 0: the 14x14 / BN 64 tile)
+    if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "conv_ring9 must be 0..7");
+    fac::set_conv_ring9(value);
+    return FAC_OK;
+  }
   if (k == "wino") {
     if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "wino must be 0..7 (bit 0: 14^2, 1: 28^2, 2: 56^2)");
     c->wino = value;
+    return FAC_OK;
+  }
+  if (k == "attn_fuse") {
+    c->attn_fuse = value != 0;
+    drop_graphs(c);
     return FAC_OK;
   }
   if (k == "conv_small") {

@@ -134,7 +134,7 @@ int fac_pipeline_join(fac_ctx* ctx, int keep, void* stream);
  * fac_debug_gemm: one encoder GEMM out[M][N] = A[M][K] . W[N][K]^T (16-bit
  * row-major operands, fp32 accumulation) with epilogue `epi` (0 fp32 + bias,
  * 1 fp32 relu, 2 16-bit gelu, 3 fp32 residual +=, 4 split-K fp32 partial
- * slabs [splits][M][N], 5 16-bit + bias), tile `variant` (-1 default, 0..3):
+ * slabs [splits][M][N], 5 16-bit + bias), tile `variant` (-1 default, 0..6):
  * the nn.Linear calls of cvit.py:28,39,50,164 in isolation. */
 #define FAC_PROFILE_STAGES 20
 int fac_debug_features_u8(fac_ctx* ctx, const uint8_t* d_in, int B, int layer, uint16_t* d_out, void* stream);

@@ -712,6 +712,37 @@ def test_small_batch_graph_follows_new_weights(sd):
     m._release()
 
 
+def test_weights_changed_in_place_or_swapped_are_used(sd):
+    """The forwards launch on the uploaded weights and then check the
+    parameters' versions and storages: a parameter changed in place, or
+    replaced by a new tensor, after the last upload is re-uploaded and the
+    forward re-run, so every result matches a model built on the new
+    weights (graph and eager batch sizes)."""
+    from fac_fake_amd.cvit import CViT
+    sdt = {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}
+    m = CViT(dtype="fp16")
+    m.load_state_dict(sdt)
+    for B in (5, 40):
+        x = torch.from_numpy(make_crops(B, seed=10 + B)).to(DEV)
+        p = (torch.arange(B) % 32).to(torch.int32).to(DEV)
+        a = m.forward_u8(x, pos_index=p).clone()
+        a2 = m.forward_u8(x, pos_index=p).clone()     # same buffers: the direct-graph path for B = 5
+        h2 = getattr(m.mlp_head, "2")
+        with torch.no_grad():
+            h2.weight.mul_(1.5)
+        b = m.forward_u8(x, pos_index=p).clone()
+        h2.bias = torch.nn.Parameter(h2.bias.detach() + 0.25)
+        c = m.forward_u8(x, pos_index=p).clone()
+        ref = CViT(dtype="fp16")
+        ref.load_state_dict(m.state_dict())
+        rc = ref.forward_u8(x, pos_index=p)
+        torch.cuda.synchronize()
+        assert torch.equal(a, a2) and not torch.equal(a, b) and not torch.equal(b, c) and torch.equal(c, rc), B
+        ref._release()
+        m.load_state_dict(sdt)
+    m._release()
+
+
 def test_forwards_on_two_streams_are_ordered(models):
     """calls on one context from different streams share its
     workspace; the C ABI makes each forward wait for the previous one on the
@@ -858,3 +889,96 @@ def test_wino_forward_vs_emulation_and_goldens(models, golden, dt, torch_threads
     fp = forward_fp32(sd, x, np.arange(4))
     got = torch.from_numpy(lg4)
     assert _rms_rel(got, fp) <= 1.6 * _rms_rel(emu, fp) + 1e-4, (_rms_rel(got, fp), _rms_rel(emu, fp))
+
+
+@pytest.mark.parametrize("B", [3, 29])
+def test_ring9_conv_is_bit_identical(models, B):
+    """Option conv_ring9 (the few-crop 14^2 / 28^2 convs with 9-slice weight
+    rings) only changes when weight slices are fetched: conv11's, conv13's,
+    conv14's and conv17's outputs and the logits are bit-identical to the
+    3-slice rings."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models["fp16"]
+    x = torch.from_numpy(make_crops(B, seed=69)).to(DEV)
+    pidx = (torch.arange(B) % 32).to(torch.int32)
+    outs = {}
+    try:
+        for v in (0, 1, 2, 4, 7):
+            m.set_option("conv_ring9", v)
+            feats = []
+            for layer, shape in ((10, (B, 28, 28, 256)), (12, (B, 14, 14, 256)), (13, (B, 14, 14, 512)),
+                                 (16, (B, 7, 7, 512))):
+                f = torch.empty(*shape, dtype=torch.float16, device=DEV)
+                _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), B, layer, f.data_ptr(), None), m._ctx, "dbg")
+                feats.append(f.view(torch.int16).cpu())
+            lg = m.forward_u8(x, pos_index=pidx)
+            torch.cuda.synchronize()
+            outs[v] = (feats, lg.cpu())
+    finally:
+        m.set_option("conv_ring9", 6)
+    for v in (1, 2, 4, 7):
+        for a, b in zip(outs[0][0], outs[v][0]):
+            assert torch.equal(a, b), v
+        assert torch.equal(outs[0][1], outs[v][1]), v
+
+
+def test_direct_graph_follows_buffer_contents(models):
+    """Small forwards on the same buffers as the previous call replay a graph
+    captured on those buffers (no copies): each replay reads the crops the
+    buffer holds at call time, and the logits / probabilities equal the eager
+    forward's, through the first (copy-graph) call, the capture and later
+    replays."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models["fp16"]
+    B = 29
+    x = torch.empty(B, 224, 224, 3, dtype=torch.uint8, device=DEV)
+    pidx = (torch.arange(B) * 5 % 32).to(torch.int32).to(DEV)
+    lg = torch.empty(B, 2, device=DEV)
+    pr = torch.empty(B, 2, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    seeds = [11, 12, 11, 13, 12, 13]
+
+    def run():
+        out = []
+        for s in seeds:
+            x.copy_(torch.from_numpy(make_crops(B, seed=s)))
+            _lib.check(lib.fac_forward_nhwc_u8(m._ctx, x.data_ptr(), B, pidx.data_ptr(), lg.data_ptr(), pr.data_ptr(),
+                                               st), m._ctx, "forward")
+            out.append((lg.clone(), pr.clone()))
+        torch.cuda.synchronize()
+        return out
+
+    got = run()
+    m.set_option("graph_max_b", 0)
+    try:
+        ref = run()
+    finally:
+        m.set_option("graph_max_b", 32)
+    for s, (a, b) in zip(seeds, zip(got, ref)):
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), s
+    assert not torch.equal(got[0][0], got[1][0])
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_fused_attention_out_proj_is_bit_identical(models, dt):
+    """Forwards of <= 32 crops run attention + to_out as one launch
+    (attn_out_gemm, option attn_fuse): logits bit-identical to the two
+    launches, for proj_splits 4 and 2, odd and even crop counts."""
+    m = models[dt]
+    try:
+        for sk in (4, 2):
+            m.set_option("proj_splits", sk)
+            for B in (1, 7, 29, 32):
+                x = torch.from_numpy(make_crops(B, seed=70 + B)).to(DEV)
+                p = (torch.arange(B) * 3 % 32).to(torch.int32).to(DEV)
+                outs = []
+                for v in (1, 0):
+                    m.set_option("attn_fuse", v)
+                    outs.append(m.forward_u8(x, pos_index=p).clone())
+                torch.cuda.synchronize()
+                assert torch.equal(outs[0], outs[1]), (sk, B)
+    finally:
+        m.set_option("attn_fuse", 1)
+        m.set_option("proj_splits", 4)
