@@ -358,6 +358,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
     const uint16_t* wnext = wsrc + (size_t)(c * 9 + WR - 1) * WSL;
     auto step = [&](auto tc) {
       constexpr int t = decltype(tc)::value;
+      constexpr int sc = t % WR;  // ring slot of slice s = 9c + t
       // WR = 9: the next chunk's halo goes out first at t = 0, ahead of slice
       // 9c+8, so the step-7 wait (which retires slice 9c+8) retires it too,
       // before step 8 reads it
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
 #pragma unroll
         for (int ct = 0; ct < CTW; ++ct) bfr[ct] = bcur[ct];
       } else {
-        const uint16_t* wb = wring + (t % WR) * WSL;
+        const uint16_t* wb = wring + sc * WSL;
 #pragma unroll
         for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
       }
@@ -857,6 +858,10 @@ static hipError_t launch_db(const uint16_t* in, const uint16_t* wpk, const float
 // prefetch (PB) too, bit 2 = conv3x3_db's 4x28 / BN 128 tile (the few-crop
 // 28^2 convs)
 static int g_ring9 = 6;
+// (Round 5, not kept: the 14x14 / BN 128 tile at B = 256 with 4- or 5-slice
+// rings cycling their slots at run time, 72 / 80 KB of LDS, still two per
+// CU: conv15-17 0.186 -> 0.196-0.201 ms.  At two workgroups per CU the slice
+// wait is covered; only the one-per-CU grids gain from depth.)
 void set_conv_ring9(int v) { g_ring9 = v; }
 static int cu_count() {
   static int cached[64] = {0};
@@ -901,7 +906,9 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
         launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       break;
     // (a two-box 14x14 workgroup needs 256+ VGPRs and spills: not built)
-    case 14128: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
+    case 14128:
+      launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      break;
     case 14192:
       if (launch_box<T, 14, 14, 192, 1, 4, 2, 2, false, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
         return hipErrorInvalidValue;

@@ -54,8 +54,6 @@ hipError_t launch_resid_layernorm(int dtype, float* x, const float* slab, int S,
 hipError_t launch_resid_cls(int dtype, const float* x, const float* slab, int S, const float* bias, uint16_t* c, int B,
                             hipStream_t st);
 hipError_t launch_attention2(int dtype, const float* qkv, uint16_t* o, int B, float scale, hipStream_t st);
-hipError_t launch_attn_out(int dtype, const float* qkv, const uint16_t* w_out, float* slab, int B, float scale,
-                           int splits, hipStream_t st);
 hipError_t launch_head_out(const float* hid, const float* w2, const float* b2, float* logits, float* probs, int B,
                            hipStream_t st);
 hipError_t launch_video_score(const float* logits, int n, float* score, hipStream_t st);
@@ -213,7 +211,6 @@ struct fac_ctx {
   static constexpr int kDirectGraphs = 8;
   int graph_max_b = 32;
   int conv_small = 1;  // option "conv_small": 28^2 / 14^2 layers on half-width column blocks when few crops
-  int attn_fuse = 1;   // option "attn_fuse": attention + to_out in one launch for <= 32 crops
   int wino = 0;        // option "wino": bit 0 / 1 / 2 = the 14^2 / 28^2 / 56^2 layers as Winograd F(2,3)
   std::vector<SmallGraph> graphs;
   hipStream_t cap_st = nullptr;
@@ -725,9 +722,6 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
   // slabs; the following kernel (residual add + next LayerNorm, or the CLS
   // finish after the last layer) sums them in split order.
   const int SK = c->proj_splits;
-  // few rows (the reference's one-video call): attention + to_out in one
-  // launch (attn_out_gemm, bit-identical to the two)
-  const bool fuse_attn = c->attn_fuse && R <= 64 && (SK == 2 || SK == 4) && c->gemm_var[2] < 0;
   for (int l = 0; l < kDepth; ++l) {
     const TLayer& T = c->tl[l];
     if (l > 0) {
@@ -735,13 +729,9 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
     }
     HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st,
                            c->gemm_var[1]));
-    if (fuse_attn) {
-      HIP_TRY(c, launch_attn_out(dt, c->qkv, T.wo, c->slab, B, scale, SK, st));
-    } else {
-      HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
-      HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st,
-                             c->gemm_var[2]));
-    }
+    HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
+    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st,
+                           c->gemm_var[2]));
     HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, T.bo, T.ln2_g, T.ln2_b, c->xn, R, st, c->ffn_ln_eps));
     HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st,
                            c->gemm_var[3]));
@@ -992,11 +982,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "wino") {
     if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "wino must be 0..7 (bit 0: 14^2, 1: 28^2, 2: 56^2)");
     c->wino = value;
-    return FAC_OK;
-  }
-  if (k == "attn_fuse") {
-    c->attn_fuse = value != 0;
-    drop_graphs(c);
     return FAC_OK;
   }
   if (k == "conv_small") {

@@ -294,8 +294,6 @@ __global__ __launch_bounds__(256) void gather_cls(const float* __restrict__ x, u
 // One wave per (crop, head); qkv is fp32 [2B][3072] laid out '(qkv h d)'.
 // attn_pair: the wave's lane holds dims lane and lane + 64 of head h of crop
 // b; o0 / o1 = the outputs of its two tokens (rows 2b, 2b+1) at those dims.
-// (One function for attention2 and attn_out_gemm: the same operations in the
-// same order, so both give the same bits.)
 __device__ __forceinline__ void attn_pair(const float* __restrict__ qkv, int b, int h, int lane, float scale,
                                           float (&o0)[2], float (&o1)[2]) {
   const float* r0 = qkv + (size_t)(2 * b) * 3072 + h * 128;
@@ -353,105 +351,11 @@ __global__ __launch_bounds__(256) void attention2(const float* __restrict__ qkv,
   }
 }
 
-// Attention + to_out (cvit.py:57-60) in one launch for few rows (M = 2B <= 64,
-// the reference's one-video call): split-K partials of o . W_out^T as
-// gemm_nt<T, EPI_PARTIAL, 64, 2, NS, 32> computes them, where each
-// workgroup first computes the attention outputs o of ITS K range (Kper / 128
-// heads, every crop) with attn_pair into an LDS A panel, instead of reading
-// o from a separate attention2 launch: the same 16-bit o values and the same
-// K order (k-tiles of 64, two MFMA k-steps each), so the same bits.  The W
-// tiles stream through the usual glds ring, issued before the attention so
-// they land meanwhile.
-template <class T, int NS>
-__global__ __launch_bounds__(256, 1) void attn_out_gemm(const float* __restrict__ qkv,
-                                                        const uint16_t* __restrict__ Wt,
-                                                        float* __restrict__ slab, int M, float scale, int Kper) {
-  constexpr int BM = 64, BN = 32, BK = 64, WM = 2, WN = 2;
-  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
-  constexpr int WSLOT = BN * BK;  // elements per W ring slot
-  constexpr int KMAX = 512;       // Kper <= 512 (split-K >= 2)
-  __shared__ __attribute__((aligned(16))) uint16_t panel[(KMAX / BK) * BM * BK];
-  __shared__ __attribute__((aligned(16))) uint16_t wring[NS * WSLOT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int n0 = blockIdx.x * BN, k0 = blockIdx.z * Kper;
-  const int nkt = Kper / BK;
-
-  // W glds: one instruction per wave per tile (32 rows x 8 pieces = 256 lanes)
-  const int wrow = 8 * wave + (lane >> 3), wpos = lane & 7;
-  const uint16_t* wsrc = Wt + (size_t)(n0 + wrow) * 1024 + k0 + ((wpos ^ ((wrow >> 1) & 7)) * 8);
-  auto issue = [&](int kt) {
-    const int slot = kt % NS, t = kt < nkt ? kt : 0;
-    glds16(wsrc + t * BK, wring + slot * WSLOT + 8 * wave * BK);
-  };
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t) issue(t);
-
-  // the A panel: o rows 0..M-1 of this K range (rows M..63 zero)
-  const int B = M >> 1, h0 = k0 >> 7, nh = Kper >> 7;
-  for (int pr = wave; pr < B * nh; pr += 4) {
-    const int b = pr / nh, hl = pr - (pr / nh) * nh;
-    float o0[2], o1[2];
-    attn_pair(qkv, b, h0 + hl, lane, scale, o0, o1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int kl = hl * 128 + lane + 64 * i, kt = kl >> 6, kk = kl & 63;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = 2 * b + j;
-        panel[(kt * BM + r) * BK + (((kk >> 3) ^ ((r >> 1) & 7)) << 3) + (kk & 7)] = T::from_f32(j ? o1[i] : o0[i]);
-      }
-    }
-  }
-  for (int e = tid; e < (BM - M) * Kper; e += 256) {
-    const int r = M + e / Kper, kl = e - (e / Kper) * Kper;
-    panel[((kl >> 6) * BM + r) * BK + (kl & 63)] = 0;
-  }
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x4)0.f;
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NS - 2) : "memory");
-  for (int kt = 0; kt < nkt; ++kt) {
-    issue(kt + NS - 1);
-    const uint16_t* sa = panel + kt * BM * BK;
-    const uint16_t* sb = wring + (kt % NS) * WSLOT;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int c = ks * 4 + (lane >> 4);
-      u16x8 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int r = wm * (BM / WM) + i * 16 + (lane & 15);
-        af[i] = *(const u16x8*)(sa + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
-      }
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int r = wn * (BN / WN) + j * 16 + (lane & 15);
-        bfr[j] = *(const u16x8*)(sb + r * BK + ((c ^ ((r >> 1) & 7)) << 3));
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = T::mfma(af[i], bfr[j], acc[i][j]);
-    }
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NS - 2) : "memory");
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M) slab[((size_t)blockIdx.z * M + m) * 1024 + n] = acc[i][j][r] + 0.f;
-      }
-  }
-}
+// (Round 5, measured and not kept: attention + to_out as one launch for
+// few rows, each workgroup computing the attention outputs of its own K
+// range into an LDS A panel before the GEMM -- bit-identical, but 17.9 us
+// against 4.9 + 5.1 for the two launches at B = 29: 32 column tiles each
+// redo the 58 (crop, head) pairs of their K range, 15 per wave in series.)
 
 // Final Linear(2048 -> 2) + per-logit sigmoid (cvit.py:164, pred_sig in
 // cvit_prediction.py:258-259); fp32 weights and activations.  One wave per crop.
@@ -688,19 +592,6 @@ hipError_t launch_gather_cls(int dtype, const float* x, uint16_t* c, int B, hipS
   dim3 grid(B);
   if (dtype == 0) gather_cls<BF16><<<grid, 256, 0, st>>>(x, c, B);
   else gather_cls<F16><<<grid, 256, 0, st>>>(x, c, B);
-  return hipGetLastError();
-}
-
-// attention + to_out split-K partials for M = 2B <= 64 rows (attn_out_gemm)
-hipError_t launch_attn_out(int dtype, const float* qkv, const uint16_t* w_out, float* slab, int B, float scale,
-                           int splits, hipStream_t st) {
-  const int M = 2 * B;
-  if (M > 64 || M <= 0 || (splits != 2 && splits != 4)) return hipErrorInvalidValue;
-  dim3 grid(1024 / 32, 1, splits);
-  if (dtype == 0)
-    attn_out_gemm<BF16, 6><<<grid, 256, 0, st>>>(qkv, w_out, slab, M, scale, 1024 / splits);
-  else
-    attn_out_gemm<F16, 6><<<grid, 256, 0, st>>>(qkv, w_out, slab, M, scale, 1024 / splits);
   return hipGetLastError();
 }
 

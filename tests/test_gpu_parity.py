@@ -959,26 +959,3 @@ def test_direct_graph_follows_buffer_contents(models):
     for s, (a, b) in zip(seeds, zip(got, ref)):
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), s
     assert not torch.equal(got[0][0], got[1][0])
-
-
-@pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_fused_attention_out_proj_is_bit_identical(models, dt):
-    """Forwards of <= 32 crops run attention + to_out as one launch
-    (attn_out_gemm, option attn_fuse): logits bit-identical to the two
-    launches, for proj_splits 4 and 2, odd and even crop counts."""
-    m = models[dt]
-    try:
-        for sk in (4, 2):
-            m.set_option("proj_splits", sk)
-            for B in (1, 7, 29, 32):
-                x = torch.from_numpy(make_crops(B, seed=70 + B)).to(DEV)
-                p = (torch.arange(B) * 3 % 32).to(torch.int32).to(DEV)
-                outs = []
-                for v in (1, 0):
-                    m.set_option("attn_fuse", v)
-                    outs.append(m.forward_u8(x, pos_index=p).clone())
-                torch.cuda.synchronize()
-                assert torch.equal(outs[0], outs[1]), (sk, B)
-    finally:
-        m.set_option("attn_fuse", 1)
-        m.set_option("proj_splits", 4)
