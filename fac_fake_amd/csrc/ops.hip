@@ -1083,7 +1083,10 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
   constexpr int HPW = (HSL + 255) / 256;                                  // glds per wave
   constexpr int WEL = 64 * 256;                                           // weight elements
   constexpr int HEL = HPW * 256 * 8;                                     // halo buffer elements
-  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * HEL];
+  constexpr int NPC_ = 2 * HH * HWD, PPL_ = (NPC_ + 255) / 256;
+  // IN == 2: the raw pixel pairs of two boxes staged in LDS (see load_raw)
+  constexpr int RSZ = IN == 2 ? 2 * PPL_ * 3 * 256 : 0;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * HEL + RSZ];
   uint16_t* const sw = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
@@ -1135,8 +1138,26 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
   constexpr int NPC = 2 * HH * HWD, PPL = (NPC + 255) / 256;
   constexpr bool F32IN = IN != 0;  // the cells are made from a raw clip while staging
   using RawT = typename std::conditional<IN == 2, uint16_t, float2>::type;
-  RawT raw[F32IN ? PPL : 1][3];
-  auto load_raw = [&](int bx) {
+  // two register sets of raw pieces (box j in set j & 1, the box loop
+  // unrolled by two so the set index is a constant): the pieces of the box
+  // after next are loaded BEFORE this box's stores, so the wait for them
+  // (one box later) never includes a box's stores -- two boxes of output
+  // stores stay in flight instead of one (round 5: the layer was bound by
+  // its stores' latency, ~3 TB/s of writes)
+  // (the in-image mask is applied when the cells are written, one box later:
+  // a select at the load would make the wave wait for the load right there)
+  // IN == 2: the pixel pairs go global -> LDS by 2-byte global_load_lds
+  // into a per-box staging area (set SET), lane-linear, each thread reading
+  // back only its own pieces; the waits for them are hand-counted (the
+  // pieces and the output stores in issue order: LLVM falls back to
+  // vmcnt(0) for a register load consumed behind stores, i.e. it would wait
+  // for the box's stores)
+  RawT raw[2][F32IN && IN != 2 ? PPL : 1][3];
+  uint16_t* const rstage = smem + WEL + 2 * HEL;
+  unsigned rok[2] = {0u, 0u};
+  auto load_raw = [&](auto setc, int bx) {
+    constexpr int SET = decltype(setc)::value;
+    rok[SET] = 0u;
     const int img = bx / bpi, rr = bx - img * bpi;
     const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
     const int clip = img / frames, f = img - clip * frames;
@@ -1148,31 +1169,35 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
       const int Y = y0 + hy, X = x0 + hx, y = 2 * (Y - pb) + pc, x = 2 * (X - pb);
       const bool ok = p < NPC && Y >= pb && X >= pb && y < H && x < W;
       const size_t off = ok ? (size_t)y * W + x : 0;  // branch-free: masked pieces read pixel 0 and are zeroed
+      rok[SET] |= ok ? 1u << j : 0u;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        if constexpr (IN == 2) {
-          const uint16_t v = *(const uint16_t*)((const uint8_t*)in_ + cbase + (size_t)c * frames * H * W + off);
-          raw[j][c] = ok ? v : (uint16_t)0;
-        } else {
-          const float2 v = *(const float2*)((const float*)in_ + cbase + (size_t)c * frames * H * W + off);
-          raw[j][c] = ok ? v : make_float2(0.f, 0.f);
-        }
+        if constexpr (IN == 2)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)((const uint8_t*)in_ + cbase + (size_t)c * frames * H * W + off),
+              (__attribute__((address_space(3))) void*)(rstage + ((SET * PPL + j) * 3 + c) * 256 + wave * 64), 2, 0, 0);
+        else
+          raw[SET][j][c] = *(const float2*)((const float*)in_ + cbase + (size_t)c * frames * H * W + off);
       }
     }
   };
-  auto store_cells = [&](uint16_t* halo) {
+  auto store_cells = [&](auto setc, uint16_t* halo) {
+    constexpr int SET = decltype(setc)::value;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int p = tid + 256 * j;
       if (p < NPC) {
         const int pc = p / (HH * HWD), rem = p - pc * (HH * HWD), hy = rem / HWD, hx = rem - (rem / HWD) * HWD;
         float2 rf[3];
+        const bool ok = (rok[SET] >> j) & 1u;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-          if constexpr (IN == 2)
-            rf[c] = make_float2((float)(raw[j][c] & 0xff), (float)(raw[j][c] >> 8));  // little-endian pixel pair
-          else
-            rf[c] = raw[j][c];
+          if constexpr (IN == 2) {
+            const uint16_t pr = rstage[((SET * PPL + j) * 3 + c) * 256 + tid];
+            rf[c] = make_float2((float)(pr & 0xff), (float)(pr >> 8));  // little-endian pixel pair
+          } else
+            rf[c] = raw[SET][j][c];
+          if (!ok) rf[c] = make_float2(0.f, 0.f);
         }
         u16x8 v;
         v[0] = T::from_f32(rf[0].x);
@@ -1188,17 +1213,32 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
     }
   };
   __syncthreads();  // weights in
-  if constexpr (F32IN) {
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if constexpr (IN == 2) {
+    // every box iteration issues one set of pieces (a dummy re-read of box
+    // 0 past the end), so the counted waits below are uniform
     if (blockIdx.x < nbox) {
-      load_raw(blockIdx.x);
-      store_cells(smem + WEL);
-      if (blockIdx.x + (int)gridDim.x < nbox) load_raw(blockIdx.x + gridDim.x);
+      load_raw(S0{}, blockIdx.x);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      store_cells(S0{}, smem + WEL);
+      load_raw(S1{}, blockIdx.x + (int)gridDim.x < nbox ? blockIdx.x + gridDim.x : 0);
+    }
+  } else if constexpr (F32IN) {
+    if (blockIdx.x < nbox) {
+      load_raw(S0{}, blockIdx.x);
+      store_cells(S0{}, smem + WEL);
+      if (blockIdx.x + (int)gridDim.x < nbox) load_raw(S1{}, blockIdx.x + gridDim.x);
     }
   } else {
     if (blockIdx.x < nbox) issue(blockIdx.x, smem + WEL);
   }
-  int it = 0;
-  for (int bx = blockIdx.x; bx < nbox; bx += gridDim.x, ++it) {
+  // box iteration `it` (parity P = it & 1: its cells came from raw set P,
+  // the next box's from set P^1; the box after next loads into set P)
+  auto box = [&](auto pc, int bx, int it) {
+    constexpr int P = decltype(pc)::value;
+    using SP = std::integral_constant<int, P>;
+    using SQ = std::integral_constant<int, P ^ 1>;
     const int img = bx / bpi, rr = bx - img * bpi;
     const int y0 = (rr / bpr) * TH, x0 = (rr - (rr / bpr) * bpr) * TW;
     uint16_t* const halo = smem + WEL + (it & 1) * HEL;
@@ -1237,6 +1277,11 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
         for (int ct = 0; ct < 2; ++ct) acc[i][ct] = T::mfma(wf[ct], pf, acc[i][ct]);
       }
     }
+    if constexpr (IN == 2)
+      load_raw(SP{}, bx + 2 * (int)gridDim.x < nbox ? bx + 2 * gridDim.x : 0);
+    else if constexpr (F32IN) {
+      if (bx + 2 * (int)gridDim.x < nbox) load_raw(SP{}, bx + 2 * gridDim.x);
+    }
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
       const int m = (wm * 7 + i) * 16 + r16, py = m / TW, px = m - (m / TW) * TW;
@@ -1251,15 +1296,26 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
       }
       *(u16x8*)o = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
     }
-    if constexpr (F32IN) {
-      // the next box's cells into the other buffer (its float pairs were
-      // fetched one box ago; this box's stores stay in flight), then the
-      // box after next's float pairs
-      if (more) {
-        store_cells(smem + WEL + ((it + 1) & 1) * HEL);
-        if (bx + 2 * (int)gridDim.x < nbox) load_raw(bx + 2 * gridDim.x);
-      }
+    if constexpr (IN == 2) {
+      // the next box's pieces (set P^1) landed: younger are the previous
+      // box's 7 stores (none before the first box), this iteration's 3 PPL
+      // pieces and this box's 7 stores
+      if (it == 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPL + 7) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PPL + 14) : "memory");
+      if (more) store_cells(SQ{}, smem + WEL + ((it + 1) & 1) * HEL);
+    } else if constexpr (F32IN) {
+      // the next box's cells into the other buffer (its pieces were fetched
+      // one box ago, before the previous box's stores, which stay in flight
+      // with this box's)
+      if (more) store_cells(SQ{}, smem + WEL + ((it + 1) & 1) * HEL);
     }
+  };
+  int it = 0;
+  for (int bx = blockIdx.x; bx < nbox; bx += 2 * gridDim.x, it += 2) {
+    box(S0{}, bx, it);
+    if (bx + (int)gridDim.x < nbox) box(S1{}, bx + gridDim.x, it + 1);
   }
 }
 
