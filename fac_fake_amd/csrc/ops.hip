@@ -1085,7 +1085,7 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
   constexpr int HEL = HPW * 256 * 8;                                     // halo buffer elements
   constexpr int NPC_ = 2 * HH * HWD, PPL_ = (NPC_ + 255) / 256;
   // IN == 2: the raw pixel pairs of two boxes staged in LDS (see load_raw)
-  constexpr int RSZ = IN == 2 ? 2 * PPL_ * 3 * 256 : 0;
+  constexpr int RSZ = IN == 2 ? 2 * PPL_ * 3 * 256 * 2 : 0;  // (one dword slot per lane and piece)
   __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * HEL + RSZ];
   uint16_t* const sw = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1147,13 +1147,14 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
   // (the in-image mask is applied when the cells are written, one box later:
   // a select at the load would make the wave wait for the load right there)
   // IN == 2: the pixel pairs go global -> LDS by 2-byte global_load_lds
-  // into a per-box staging area (set SET), lane-linear, each thread reading
-  // back only its own pieces; the waits for them are hand-counted (the
+  // into a per-box staging area (set SET), lane-linear in dword slots (the
+  // LDS side of a sub-dword LDS-DMA load is M0 + 4 * lane), each thread
+  // reading back only its own pieces; the waits for them are hand-counted (the
   // pieces and the output stores in issue order: LLVM falls back to
   // vmcnt(0) for a register load consumed behind stores, i.e. it would wait
   // for the box's stores)
   RawT raw[2][F32IN && IN != 2 ? PPL : 1][3];
-  uint16_t* const rstage = smem + WEL + 2 * HEL;
+  uint32_t* const rstage = (uint32_t*)(smem + WEL + 2 * HEL);
   unsigned rok[2] = {0u, 0u};
   auto load_raw = [&](auto setc, int bx) {
     constexpr int SET = decltype(setc)::value;
@@ -1193,7 +1194,7 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
           if constexpr (IN == 2) {
-            const uint16_t pr = rstage[((SET * PPL + j) * 3 + c) * 256 + tid];
+            const uint32_t pr = rstage[((SET * PPL + j) * 3 + c) * 256 + tid] & 0xffffu;
             rf[c] = make_float2((float)(pr & 0xff), (float)(pr >> 8));  // little-endian pixel pair
           } else
             rf[c] = raw[SET][j][c];
