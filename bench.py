@@ -231,7 +231,9 @@ def layer_roofline_ms(run, dtype: str) -> dict:
     at these batch sizes are mostly HBM-bound (arithmetic intensity under the
     ~312 FLOP/B ridge), so the MFMA-only fraction understates them.
     ResNet's conv1 with its fused max-pool (conv_s2d4_mp) likewise counts as
-    one op (the conv's FLOPs, the input and the pooled output's bytes)."""
+    one op (the conv's FLOPs, the input and the pooled output's bytes), and
+    so does S3D's base.0 run as one launch (ops.s3d_base0_u8: both halves'
+    FLOPs, the uint8 clip and the temporal output's bytes)."""
     from fac_fake_amd import ops, resvitkan, s3d
     recs = []
     orig_call, orig_pool, orig_sep = ops.ConvLayer.__call__, ops.pool, ops.max_pool_sep
@@ -256,6 +258,17 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         out = orig_s2dc(layer, clip, **kw)
         M = out.numel() // layer.cout
         recs.append((2.0 * M * layer.cout * layer.g.kh * layer.g.kw * layer.cin,
+                     clip.element_size() * clip.numel() + 2.0 * out.numel()))
+        return out
+
+    orig_b0 = ops.s3d_base0_u8
+
+    def b0_hook(spatial, temporal, clip, **kw):   # S3D's base.0, both halves in one launch: clip in, output out
+        out = orig_b0(spatial, temporal, clip, **kw)
+        Mt = out.numel() // temporal.cout
+        Ms = Mt * 2   # the spatial half's positions: 16 frames -> 8 (temporal stride 2)
+        recs.append((2.0 * Ms * spatial.cout * spatial.g.kh * spatial.g.kw * spatial.cin
+                     + 2.0 * Mt * temporal.cout * temporal.g.kd * temporal.cin,
                      clip.element_size() * clip.numel() + 2.0 * out.numel()))
         return out
 
@@ -295,6 +308,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
 
     ops.ConvLayer.__call__ = conv_hook
     ops.conv_s2d4_clip = s2dc_hook
+    ops.s3d_base0_u8 = b0_hook
     ops.conv_dual = resvitkan.conv_dual = dual_hook
     ops.bottleneck_pw2 = resvitkan.bottleneck_pw2 = pw2_hook
     ops.pool = resvitkan.pool = s3d.pool = pool_hook
@@ -305,6 +319,7 @@ def layer_roofline_ms(run, dtype: str) -> dict:
     finally:
         ops.ConvLayer.__call__ = orig_call
         ops.conv_s2d4_clip = orig_s2dc
+        ops.s3d_base0_u8 = orig_b0
         ops.conv_dual = resvitkan.conv_dual = orig_dual
         ops.bottleneck_pw2 = resvitkan.bottleneck_pw2 = orig_pw2
         ops.pool = resvitkan.pool = s3d.pool = orig_pool

@@ -1320,6 +1320,288 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
   }
 }
 
+// ---- s3d_base0 (round 5): S3D's base.0 -- SepConv3d(3,
+// 64, k 7, s 2, p 3) = the (1,7,7)/(1,2,2) spatial conv + BN + ReLU, then the
+// (7,1,1)/(2,1,1) temporal conv + BN + ReLU (model.py:18,63-82) -- in ONE
+// launch from the uint8 clip.  conv_s2d4 -> conv_tk2<2,7,2> wrote the
+// 16-frame half-resolution map ([n][16][56][56][64], 6.4 MB per clip) and
+// read it back: 9.9 GB of HBM per 1536-clip step between the two halves.
+// Here a workgroup takes a unit = (clip, 2 x 8 output positions) through
+// both halves with the 16-frame map of its 16 positions in LDS:
+//  A. spatial: wave w computes frames 2w, 2w+1 -- conv_s2d4's 4x4 conv over
+//     16-channel space-to-depth cells, its weight layout, k-step order and
+//     transposed MFMAs (rows = channels), so the same sums -- from the
+//     unit's cell image (16 frames x 2 pixel rows x 5 x 11 cells);
+//  B. bias + ReLU -> 16-bit S image [chunk][frame][position][32 channels]
+//     (conv_tk2's slice layout and swizzle); the next unit's cells are
+//     written meanwhile (its pixel pairs were loaded at the unit's start);
+//  C. temporal: wave (fp, h) computes output frames 2fp, 2fp+1 x channels
+//     32h .. 32h+31 exactly as conv_tk2<2,7,2> does (chunk outer, tap inner,
+//     zero-padded taps skipped), and stores 16 bytes per lane from registers.
+// Bit-identical to the two launches (test_s3d_base0_fused_equals_two_launches).
+// LDS: spatial weights 32 KB, temporal weights 56 KB, S image 32 KB, cell
+// image 30 KB: one 512-thread workgroup per CU, persistent over units.
+#ifdef B0_STAMPS
+// tools/ubench/b0_ubench.hip: s_memtime of wave w of workgroup x in its k-th
+// unit at: 0 unit start, 1 after barrier A, 2 spatial MFMAs done, 3 after
+// barrier B, 4 phase B done, 5 after barrier C, 6 temporal MFMAs done, 7 stored
+__device__ unsigned long long b0_st[8][16][8][8];
+#define B0_STAMP(k)                                                                               \
+  do {                                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    unsigned long long t_;                                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                    \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    const int k_ = (u - (int)blockIdx.x) / (int)gridDim.x;                                        \
+    if (blockIdx.x < 8 && lane == 0 && k_ < 16) b0_st[blockIdx.x][k_][wave][(k)] = t_;            \
+  } while (0)
+#else
+#define B0_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
+template <class T>
+__global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ clip,
+                                                    const uint16_t* __restrict__ wsp, const float* __restrict__ bsp,
+                                                    int kps, const uint16_t* __restrict__ wtm,
+                                                    const float* __restrict__ btm, int kpt,
+                                                    uint16_t* __restrict__ out, int nunits, int H, int W, int pb,
+                                                    int relu_s, int relu_t) {
+  constexpr int T_IN = 16, T_OUT = 8, HO = 56, WO = 56;   // frames in / out, half-resolution map
+  constexpr int BH = 2, BW = 8;                            // output box (16 positions = one MFMA column tile)
+  constexpr int CH = BH + 3, CW = BW + 3, RPX = 12;        // cell rows / cols of a box, row pitch (16-B slots)
+  constexpr int FSL = 2 * CH * RPX;                        // cell slots per frame (2 pixel rows per cell)
+  constexpr int NPC = T_IN * 2 * CH * CW, PPL = (NPC + 511) / 512;  // cell pieces per unit / per thread
+  constexpr int KD = 7, SD = 2, PD = 3, NF = SD + KD;      // temporal conv
+  constexpr int WS_EL = 64 * 256, WT_EL = KD * 2 * 2048, S_EL = 2 * T_IN * 16 * 32, C_EL = T_IN * FSL * 8;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WS_EL + WT_EL + S_EL + C_EL];
+  __shared__ float bias_s[64], bias_t[64];
+  uint16_t* const sws = smem;
+  uint16_t* const swt = smem + WS_EL;
+  uint16_t* const simg = swt + WT_EL;
+  uint16_t* const cells = simg + S_EL;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  constexpr int BPR = WO / BW, BPC = (HO / BH) * BPR;      // boxes per row / per clip
+
+  // weights: both in conv_s2d4's / conv_tk2's fragment layout
+  // [k-step][ct][g][r16][8] (row i of tile ct = channel 32 (ct >> 1) + 8 (i >> 2) + 4 (ct & 1) + (i & 3))
+  for (int c = tid; c < 64 * 32; c += 512) {
+    const int n = c >> 5, k8 = c & 31;
+    const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
+    *(u16x8*)(sws + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) = *(const u16x8*)(wsp + (size_t)n * kps + k8 * 8);
+  }
+  for (int c = tid; c < 64 * KD * 2 * 4; c += 512) {
+    const int n = c / (KD * 2 * 4), k8 = c - n * (KD * 2 * 4);
+    const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
+    *(u16x8*)(swt + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) = *(const u16x8*)(wtm + (size_t)n * kpt + k8 * 8);
+  }
+  if (tid < 64) {
+    bias_s[tid] = bsp ? bsp[tid] : 0.f;
+    bias_t[tid] = btm ? btm[tid] : 0.f;
+  }
+
+  // the pixel pairs of a unit's cell pieces: piece p = tid + 512 j ->
+  // (frame f, pixel row pc of the cell, cell row hy, cell column hx); per
+  // colour plane one 2-byte pixel pair (x, x+1) of pixel row y
+  // Each pixel pair comes in the aligned dword that holds it (w % 4 == 0, x
+  // even: never past the row), the pair's half recorded in rsh: no ALU touches
+  // a loaded value before phase B (the compiler would wait for the load there)
+  // Two register sets, the unit loop unrolled by two so the set is a
+  // constant: a unit's pixels are loaded two units ahead (one unit of HBM
+  // latency cover instead of one spatial phase).
+  uint32_t raw[2][PPL][3];
+  unsigned rok[2] = {0u, 0u}, rsh[2] = {0u, 0u};
+  auto load_raw = [&](auto setc, int u) {
+    constexpr int SET = decltype(setc)::value;
+    const int n = u / BPC, b = u - n * BPC;
+    const int y0 = (b / BPR) * BH, x0 = (b - (b / BPR) * BPR) * BW;
+    rok[SET] = 0u;
+    rsh[SET] = 0u;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = tid + 512 * j;
+      const int f = p / (2 * CH * CW), r1 = p - f * (2 * CH * CW);
+      const int pc = r1 / (CH * CW), r2 = r1 - pc * (CH * CW), hy = r2 / CW, hx = r2 - hy * CW;
+      const int Y = y0 + hy, X = x0 + hx, y = 2 * (Y - pb) + pc, x = 2 * (X - pb);
+      const bool ok = p < NPC && Y >= pb && X >= pb && y < H && x < W;
+      const size_t off = ok ? ((size_t)(n * 3) * T_IN + f) * H * W + (size_t)y * W + x : 0;
+      rok[SET] |= ok ? 1u << j : 0u;
+      rsh[SET] |= ((unsigned)(off >> 1) & 1u) << j;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        raw[SET][j][c] = *(const uint32_t*)(clip + (((size_t)c * T_IN * H * W + off) & ~(size_t)3));
+    }
+  };
+  auto store_cells = [&](auto setc) {
+    constexpr int SET = decltype(setc)::value;
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = tid + 512 * j;
+      if (p < NPC) {
+        const int f = p / (2 * CH * CW), r1 = p - f * (2 * CH * CW);
+        const int pc = r1 / (CH * CW), r2 = r1 - pc * (CH * CW), hy = r2 / CW, hx = r2 - hy * CW;
+        const bool ok = (rok[SET] >> j) & 1u;
+        const unsigned sh = ((rsh[SET] >> j) & 1u) * 16u;
+        u16x8 v;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const unsigned pr = raw[SET][j][c] >> sh;
+          const float lo = ok ? (float)(pr & 0xff) : 0.f, hi = ok ? (float)((pr >> 8) & 0xff) : 0.f;
+          v[c] = T::from_f32(lo);
+          v[4 + c] = T::from_f32(hi);
+        }
+        v[3] = 0;
+        v[7] = 0;
+        *(u16x8*)(cells + ((f * 2 + pc) * CH * RPX + hy * RPX + hx) * 8) = v;
+      }
+    }
+  };
+
+  // spatial fragment offsets: lane (g, r16) = position (py, px) of the box,
+  // piece g & 1 of the cell at tap column offset g >> 1 (conv_s2d4)
+  const int py = r16 >> 3, px = r16 & 7;
+  const int cbo = ((g & 1) * CH + py) * RPX + px + (g >> 1);
+  // S image: chunk c, frame d, position r16, channel piece q at ((c * 16 + d) * 16 + r16) * 32 + ((q ^ ((r16 >> 1) & 2)) << 3)
+  const int rdoff = r16 * 32 + ((g ^ ((r16 >> 1) & 2)) << 3);
+  const int fp = wave & 3, hh = wave >> 2;
+  const int d0 = 2 * fp * SD - PD;
+  const uint16_t* const wl = swt + (hh * 2 * 4 + g) * 128 + r16 * 8;
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  const int G = gridDim.x;
+  if ((int)blockIdx.x < nunits) {
+    load_raw(S0{}, blockIdx.x);
+    store_cells(S0{});
+    load_raw(S1{}, (int)blockIdx.x + G < nunits ? blockIdx.x + G : 0);
+  }
+  // unit iteration of parity P: its cells came from set P; the next unit's
+  // are written from set P^1 (loaded one unit ago), and the unit after next
+  // loads into set P
+  auto unit = [&](auto pc, int u) {
+    constexpr int P = decltype(pc)::value;
+    using SP = std::integral_constant<int, P>;
+    using SQ = std::integral_constant<int, P ^ 1>;
+    const int un = u + G;
+    B0_STAMP(0);
+    // (past the end: a dummy load of unit 0, so the compiler's wait counts
+    // are the same on every path)
+    load_raw(SP{}, u + 2 * G < nunits ? u + 2 * G : 0);
+    // A: cells of u written, the S image free.  The three phase barriers
+    // order LDS only (no global data passes between waves): lgkmcnt +
+    // s_barrier, not __syncthreads, whose fence would also wait for the
+    // pixel loads just issued and the previous unit's output stores
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    B0_STAMP(1);
+    // ---- A: spatial conv of frames 2w, 2w+1
+    f32x4 sacc[2][4];
+#pragma unroll
+    for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) sacc[fi][ct] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      u16x8 wf[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) wf[ct] = *(const u16x8*)(sws + (((s * 4 + ct) * 4 + g) * 16 + r16) * 8);
+      const int so = (s >> 1) * RPX + (s & 1) * 2;
+#pragma unroll
+      for (int fi = 0; fi < 2; ++fi) {
+        const u16x8 pf = *(const u16x8*)(cells + ((2 * wave + fi) * FSL + cbo + so) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) sacc[fi][ct] = T::mfma(wf[ct], pf, sacc[fi][ct]);
+      }
+    }
+    B0_STAMP(2);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B: every wave is done with the cells
+    B0_STAMP(3);
+    // ---- B: S image (bias + ReLU, 16-bit) and the next unit's cells
+#pragma unroll
+    for (int fi = 0; fi < 2; ++fi) {
+      const int d = 2 * wave + fi;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {  // chunk c = channels 32c .. 32c+31 = tiles 2c, 2c+1
+        u16x4 q[2];
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+          f32x4 v;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            const float x = sacc[fi][2 * c + cc][jj] + bias_s[32 * c + 8 * g + 4 * cc + jj];
+            v[jj] = relu_s ? relu(x) : x;
+          }
+          q[cc] = T::pack4(v);
+        }
+        *(u16x8*)(simg + (c * T_IN + d) * 512 + rdoff) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+    // the next unit's pixels (set P^1, loaded one unit ago) have landed: at
+    // most this unit's PPL x 3 loads and the previous unit's 2 output stores
+    // are younger (an intrinsic, not asm, so the compiler's own wait
+    // bookkeeping sees it and adds no vmcnt(0) of its own)
+    static_assert(3 * PPL + 2 < 16, "vmcnt immediate");
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (3 * PPL + 2));
+    if (un < nunits) store_cells(SQ{});
+    B0_STAMP(4);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // C: the S image is complete
+    B0_STAMP(5);
+    // ---- C: temporal conv, conv_tk2<2, 7, 2>'s arithmetic
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[j][0] = acc[j][1] = (f32x4)0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint16_t* cur = simg + c * T_IN * 512 + rdoff;
+      u16x8 pxf[NF], wf[KD][2];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int d = d0 + f;
+        pxf[f] = (unsigned)d < (unsigned)T_IN ? *(const u16x8*)(cur + d * 512) : (u16x8)0;
+      }
+#pragma unroll
+      for (int t = 0; t < KD; ++t)
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) wf[t][cc] = *(const u16x8*)(wl + (t * 2 + c) * 2048 + cc * 512);
+#pragma unroll
+      for (int t = 0; t < KD; ++t)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int f = j * SD + t;
+          if ((unsigned)(d0 + f) < (unsigned)T_IN) {
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) acc[j][cc] = T::mfma(wf[t][cc], pxf[f], acc[j][cc]);
+          }
+        }
+    }
+    B0_STAMP(6);
+    const int n = u / BPC, b = u - n * BPC;
+    const int oy = (b / BPR) * BH + py, ox = (b - (b / BPR) * BPR) * BW + px;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      uint16_t* o = out + (((size_t)n * T_OUT + 2 * fp + j) * (HO * WO) + oy * WO + ox) * 64 + hh * 32 + 8 * g;
+      u16x4 q2[2];
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        f32x4 v;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float x = acc[j][cc][qq] + bias_t[hh * 32 + 8 * g + 4 * cc + qq];
+          v[qq] = relu_t ? relu(x) : x;
+        }
+        q2[cc] = T::pack4(v);
+      }
+      *(u16x8*)o = __builtin_shufflevector(q2[0], q2[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    B0_STAMP(7);
+  };
+  for (int u = blockIdx.x; u < nunits; u += 2 * G) {
+    unit(S0{}, u);
+    if (u + G < nunits) unit(S1{}, u + G);
+  }
+}
+
 // ---- conv_s2d4_mp: conv_s2d4 (+ bias + ReLU) with the MaxPool2d(3, 2, 1)
 // that follows it in ResNet-50 (ResVitKan.py:187's torchvision resnet50:
 // conv1 -> bn1 -> relu -> maxpool) fused in, so the 112^2 conv output never
@@ -2943,6 +3225,49 @@ int fac_conv_s2d4_clip(const fac_conv_desc* d, const float* clip, int h, int w, 
 
 int fac_conv_s2d4_clip_u8(const fac_conv_desc* d, const uint8_t* clip, int h, int w, int pad_before, void* stream) {
   return conv_s2d4_clip_impl(d, clip, true, h, w, pad_before, stream);
+}
+
+int fac_s3d_base0_u8(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, const uint8_t* clip, int h, int w,
+                     int pad_before, void* stream) {
+  using namespace fac;
+  if (!sdsc || !tdsc || !clip || !sdsc->weight || !tdsc->weight || !tdsc->out || sdsc->dtype != tdsc->dtype ||
+      (sdsc->dtype != FAC_DTYPE_BF16 && sdsc->dtype != FAC_DTYPE_F16))
+    return FAC_ERR_ARG;
+  if (((sdsc->flags | tdsc->flags) & ~FAC_CONV_RELU) != 0 || pad_before < 0) return FAC_ERR_ARG;
+  int cps, kps, cpt, kpt;
+  fac_conv_weight_layout(sdsc->cout, sdsc->cin, sdsc->kd, sdsc->kh, sdsc->kw, &cps, &kps);
+  fac_conv_weight_layout(tdsc->cout, tdsc->cin, tdsc->kd, tdsc->kh, tdsc->kw, &cpt, &kpt);
+  // the spatial half as fac_conv_s2d4_clip_u8 takes it (4x4/1 over 16-channel
+  // cells of 16 frames, a 56 x 56 output), the temporal half as conv_tk2<2,7,2>
+  const bool sp = sdsc->kd == 1 && sdsc->kh == 4 && sdsc->kw == 4 && sdsc->sd == 1 && sdsc->sh == 1 && sdsc->sw == 1 &&
+                  sdsc->pd == 0 && sdsc->ph == 0 && sdsc->pw == 0 && sdsc->cin == 16 && sdsc->cout == 64 &&
+                  sdsc->k_pad == kps && kps == 256 && sdsc->d == 16 && sdsc->od == 16 && sdsc->oh == 56 &&
+                  sdsc->ow == 56 && sdsc->h == 59 && sdsc->w == 59 && h % 2 == 0 && w % 2 == 0 &&
+                  sdsc->h >= h / 2 + pad_before && sdsc->w >= w / 2 + pad_before;
+  const bool tp = tdsc->kd == 7 && tdsc->kh == 1 && tdsc->kw == 1 && tdsc->sd == 2 && tdsc->sh == 1 && tdsc->sw == 1 &&
+                  tdsc->pd == 3 && tdsc->ph == 0 && tdsc->pw == 0 && tdsc->cin == 64 && tdsc->cout == 64 &&
+                  tdsc->k_pad == kpt && kpt == 7 * 64 && tdsc->n == sdsc->n && tdsc->d == 16 && tdsc->h == 56 &&
+                  tdsc->w == 56 && tdsc->od == 8 && tdsc->oh == 56 && tdsc->ow == 56 && tdsc->ldo == 64 &&
+                  tdsc->c_off == 0;
+  if (!sp || !tp || sdsc->n <= 0) return FAC_ERR_SHAPE;
+  if ((long long)sdsc->n * 16 * 3 * h * w >= (1LL << 40)) return FAC_ERR_SHAPE;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const int nunits = sdsc->n * (56 / 2) * (56 / 8);
+  const int grid = std::min(nunits, ncu);
+  const int rs = (sdsc->flags & FAC_CONV_RELU) != 0, rt = (tdsc->flags & FAC_CONV_RELU) != 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (sdsc->dtype == FAC_DTYPE_BF16)
+    s3d_base0<BF16><<<grid, 512, 0, st>>>(clip, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
+                                          (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out,
+                                          nunits, h, w, pad_before, rs, rt);
+  else
+    s3d_base0<F16><<<grid, 512, 0, st>>>(clip, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
+                                         (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out,
+                                         nunits, h, w, pad_before, rs, rt);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 
 int fac_conv_nd_split(const fac_conv_desc* d, void* out1, int ldo1, int split1, void* out2, int ldo2, int split2,

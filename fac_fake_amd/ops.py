@@ -433,6 +433,45 @@ def conv_s2d4_clip(layer: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2,
     return out
 
 
+def s3d_base0_u8(spatial: ConvLayer, temporal: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2,
+                 pad_after: int = 1) -> torch.Tensor:
+    """S3D's base.0 in one launch (fac_s3d_base0_u8): ``temporal(
+    conv_s2d4_clip(spatial, clip))`` for a uint8 clip batch [N, 3, 16, 112,
+    112], both halves + ReLU, without the 16-frame half-resolution map going
+    through HBM; bit-identical to the two launches.  -> [N, 8, 56, 56, 64]."""
+    if clip.dtype != torch.uint8 or clip.dim() != 5 or clip.shape[1] != 3 or not clip.is_contiguous():
+        raise ValueError(f"expected a contiguous uint8 clip [N,3,16,H,W], got {clip.dtype} {tuple(clip.shape)}")
+    n, _, t, h, w = clip.shape
+    hc, wc = h // 2 + pad_before + pad_after, w // 2 + pad_before + pad_after
+    od, oh, ow = spatial.out_dims(t, hc, wc)
+    g = spatial.g
+    sd = ConvDesc()
+    sd.dtype = _lib.DTYPES[spatial.dtype]
+    sd.n, sd.d, sd.h, sd.w, sd.cin = n, t, hc, wc, spatial.cin_p
+    sd.weight, sd.bias = spatial.w.data_ptr(), spatial.b.data_ptr()
+    sd.cout, sd.k_pad = spatial.cout, spatial.k_pad
+    sd.kd, sd.kh, sd.kw, sd.sd, sd.sh, sd.sw = g.kd, g.kh, g.kw, g.sd, g.sh, g.sw
+    sd.pd, sd.ph, sd.pw = g.pd, g.ph, g.pw
+    sd.od, sd.oh, sd.ow = od, oh, ow
+    sd.ldo, sd.flags = spatial.cout, RELU
+    tod, toh, tow = temporal.out_dims(od, oh, ow)
+    out = torch.empty(n, tod, toh, tow, temporal.cout, device=clip.device, dtype=TORCH16[temporal.dtype])
+    tg = temporal.g
+    td = ConvDesc()
+    td.dtype = _lib.DTYPES[temporal.dtype]
+    td.n, td.d, td.h, td.w, td.cin = n, od, oh, ow, temporal.cin_p
+    td.weight, td.bias = temporal.w.data_ptr(), temporal.b.data_ptr()
+    td.cout, td.k_pad = temporal.cout, temporal.k_pad
+    td.kd, td.kh, td.kw, td.sd, td.sh, td.sw = tg.kd, tg.kh, tg.kw, tg.sd, tg.sh, tg.sw
+    td.pd, td.ph, td.pw = tg.pd, tg.ph, tg.pw
+    td.od, td.oh, td.ow = tod, toh, tow
+    td.out, td.ldo, td.c_off = out.data_ptr(), temporal.cout, 0
+    td.flags = RELU
+    _lib.check(_lib.load().fac_s3d_base0_u8(ctypes.byref(sd), ctypes.byref(td), clip.data_ptr(), h, w, pad_before,
+                                            _stream(clip)), None, "fac_s3d_base0_u8")
+    return out
+
+
 def s2d_weight(w: torch.Tensor) -> torch.Tensor:
     """[co, 3, 7, 7] stride-2 pad-3 kernel -> [co, 16, 4, 4] stride-1 kernel over
     fac_pack_input_s2d cells: w'[o][(dy*2+dx)*4 + c][ty][tx] = w[o][c][2ty+dy-1][2tx+dx-1].

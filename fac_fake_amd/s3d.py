@@ -64,6 +64,8 @@ class S3D(nn.Module):
         self.SRM_net = SRM_net
         self.dtype_name = dtype
         self._srm = SRM_net == "yes"
+        # base.0 of a uint8 16 x 112 x 112 clip as one launch (ops.s3d_base0_u8)
+        self.fuse_base0 = True
         for name, shape, kind in s3d_param_specs(num_class, self._srm):
             *path, leaf = name.split(".")
             mod = self
@@ -245,10 +247,16 @@ class S3D(nn.Module):
             y = self._srm_conv(y, relu=False, out=s)
         for kind, L in self._layers:
             if kind == "sep_s2d":
-                # the raw fp32 clip (`_pack`): the space-to-depth packing runs
+                # the raw clip (`_pack`): the space-to-depth packing runs
                 # inside the conv's halo staging (ops.conv_s2d4_clip); packed
-                # cells (ops.pack_input_s2d) still take the plain conv
-                y = L[1](ops.conv_s2d4_clip(L[0], y) if y.dtype in (torch.float32, torch.uint8) else L[0](y))
+                # cells (ops.pack_input_s2d) still take the plain conv.  A
+                # uint8 16 x 112 x 112 clip runs both halves as one launch
+                # (ops.s3d_base0_u8; fuse_base0 = False: the two launches)
+                if y.dtype == torch.uint8 and self.fuse_base0 and tuple(y.shape[2:]) == (16, 112, 112) and \
+                        _lib.exports("fac_s3d_base0_u8"):
+                    y = ops.s3d_base0_u8(L[0], L[1], y)
+                else:
+                    y = L[1](ops.conv_s2d4_clip(L[0], y) if y.dtype in (torch.float32, torch.uint8) else L[0](y))
             elif kind == "sep":
                 y = L[1](L[0](y))
             elif kind == "basic":

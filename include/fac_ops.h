@@ -175,6 +175,17 @@ int fac_conv_s2d4_clip(const fac_conv_desc* desc, const float* clip, int h, int 
 int fac_conv_s2d4_clip_u8(const fac_conv_desc* desc, const uint8_t* clip, int h, int w, int pad_before,
                           void* stream);
 
+/* S3D's base.0 (SepConv3d(3, 64, k 7, s 2, p 3), model.py:18,63-82) in one
+ * launch from a uint8 clip batch [n][3][16][h][w] with h / 2 = w / 2 = 56
+ * (the 112 x 112 clips of S3D-test.py): `sdesc` is the spatial half as
+ * fac_conv_s2d4_clip_u8 takes it (the space-to-depth 4x4 conv, cout 64),
+ * `tdesc` the temporal (7,1,1)/(2,1,1) conv (64 -> 64, 16 -> 8 frames, its
+ * `in` unused) whose `out` receives [n][8][56][56][64].  The 16-frame
+ * half-resolution map between the two never goes through HBM; the output is
+ * bit-identical to fac_conv_s2d4_clip_u8 followed by fac_conv_nd(tdesc). */
+int fac_s3d_base0_u8(const fac_conv_desc* sdesc, const fac_conv_desc* tdesc, const uint8_t* clip, int h, int w,
+                     int pad_before, void* stream);
+
 /* KANLinear forward (CViT-main/ResVitKan/kan.py:189-206), fp32:
  *   y = silu(x) · base_weightᵀ + b_splines(x) · (spline_weight ⊙ spline_scaler)ᵀ
  * with order-3 B-spline bases over the per-feature knot vector `grid`

@@ -740,3 +740,32 @@ def _split_case(g, n, d, h, w, cin, widths, dt):
     torch.cuda.synchronize()
     assert torch.equal(out[..., :widths[0]], r0) and out[..., widths[0]:].abs().max() == 0
     assert torch.equal(h1, r1) and torch.equal(h2, r2)
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_s3d_base0_fused_equals_two_launches(s3d_models, dt):
+    """base.0 (SepConv3d 3->64, k 7, s 2) of a uint8
+    16 x 112 x 112 clip batch as one launch (fac_s3d_base0_u8) is
+    bit-identical to conv_s2d4_clip_u8 + the temporal conv_tk2, for a batch
+    whose units do not divide the persistent grid, and the whole S3D forward
+    with it equals the forward without it."""
+    from fac_fake_amd import ops
+    from fac_fake_amd.weights import s3d_clips
+    m = s3d_models[("no", dt)]
+    x = torch.from_numpy(s3d_clips(3, 16, 112, seed=77)).to(DEV).to(torch.uint8)
+    m._pack(x)
+    kind, L = m._layers[0]
+    assert kind == "sep_s2d"
+    fused = ops.s3d_base0_u8(L[0], L[1], x.contiguous())
+    two = L[1](ops.conv_s2d4_clip(L[0], x.contiguous()))
+    torch.cuda.synchronize()
+    assert fused.shape == two.shape == (3, 8, 56, 56, 64)
+    assert torch.equal(fused.view(torch.int16), two.view(torch.int16))
+    a = m(x)
+    m.fuse_base0 = False
+    try:
+        b = m(x)
+    finally:
+        m.fuse_base0 = True
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

@@ -21,11 +21,16 @@ def main():
     ap.add_argument("--B", type=int, default=384)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--u8", action="store_true", help="uint8 clips (decoded frames: base.0 as one launch)")
+    ap.add_argument("--no-fuse", action="store_true", help="with --u8: base.0 as two launches")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     m = S3D(1, "no", dtype=a.dtype)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, False).items()})
     clips = torch.from_numpy(s3d_clips(a.B, 16, 112, seed=3)).to(dev)
+    if a.u8:
+        clips = clips.to(torch.uint8)
+    m.fuse_base0 = not a.no_fuse
     for _ in range(a.reps):
         m(clips)
         torch.cuda.synchronize()
