@@ -1333,18 +1333,20 @@ __global__ __launch_bounds__(256, 2) void conv_s2d4(const void* __restrict__ in_
 //     transposed MFMAs (rows = channels), so the same sums -- from the
 //     unit's cell image (16 frames x 2 pixel rows x 5 x 11 cells);
 //  B. bias + ReLU -> 16-bit S image [chunk][frame][position][32 channels]
-//     (conv_tk2's slice layout and swizzle); the next unit's cells are
-//     written meanwhile (its pixel pairs were loaded at the unit's start);
+//     (conv_tk2's slice layout and swizzle);
 //  C. temporal: wave (fp, h) computes output frames 2fp, 2fp+1 x channels
 //     32h .. 32h+31 exactly as conv_tk2<2,7,2> does (chunk outer, tap inner,
-//     zero-padded taps skipped), and stores 16 bytes per lane from registers.
+//     zero-padded taps skipped), writes the next unit's cells behind those
+//     MFMAs (its pixel pairs were loaded a unit earlier) and stores 16 bytes
+//     per lane from registers.
 // Bit-identical to the two launches (test_s3d_base0_fused_equals_two_launches).
 // LDS: spatial weights 32 KB, temporal weights 56 KB, S image 32 KB, cell
 // image 30 KB: one 512-thread workgroup per CU, persistent over units.
 #ifdef B0_STAMPS
 // tools/ubench/b0_ubench.hip: s_memtime of wave w of workgroup x in its k-th
-// unit at: 0 unit start, 1 after barrier A, 2 spatial MFMAs done, 3 after
-// barrier B, 4 phase B done, 5 after barrier C, 6 temporal MFMAs done, 7 stored
+// unit at: 0 unit start, 1 after barrier A, 2 spatial MFMAs done (+ the pixel
+// loads issued), 3 = 2, 4 S frames written, 5 after barrier C, 6 temporal
+// MFMAs + next cells done, 7 stored
 __device__ unsigned long long b0_st[8][16][8][8];
 #define B0_STAMP(k)                                                                               \
   do {                                                                                            \
@@ -1370,8 +1372,12 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
                                                     int relu_s, int relu_t) {
   constexpr int T_IN = 16, T_OUT = 8, HO = 56, WO = 56;   // frames in / out, half-resolution map
   constexpr int BH = 2, BW = 8;                            // output box (16 positions = one MFMA column tile)
-  constexpr int CH = BH + 3, CW = BW + 3, RPX = 12;        // cell rows / cols of a box, row pitch (16-B slots)
-  constexpr int FSL = 2 * CH * RPX;                        // cell slots per frame (2 pixel rows per cell)
+  // cell rows / cols of a box; row pitch RPX and pixel-row plane pitch PP
+  // (16-byte slots) chosen by simulating the ds_read_b128 lane groups of the
+  // spatial fragment reads over the 8 k-steps: 2-way at most (conflict-free
+  // needs 176 slots per frame, 15 KB more than the LDS has left)
+  constexpr int CH = BH + 3, CW = BW + 3, RPX = 11, PP = 56;
+  constexpr int FSL = 2 * PP;                              // cell slots per frame (2 pixel rows per cell)
   constexpr int NPC = T_IN * 2 * CH * CW, PPL = (NPC + 511) / 512;  // cell pieces per unit / per thread
   constexpr int KD = 7, SD = 2, PD = 3, NF = SD + KD;      // temporal conv
   constexpr int WS_EL = 64 * 256, WT_EL = KD * 2 * 2048, S_EL = 2 * T_IN * 16 * 32, C_EL = T_IN * FSL * 8;
@@ -1407,26 +1413,38 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
   // colour plane one 2-byte pixel pair (x, x+1) of pixel row y
   // Each pixel pair comes in the aligned dword that holds it (w % 4 == 0, x
   // even: never past the row), the pair's half recorded in rsh: no ALU touches
-  // a loaded value before phase B (the compiler would wait for the load there)
+  // a loaded value before the cells are written (the compiler would wait for
+  // the load there)
   // Two register sets, the unit loop unrolled by two so the set is a
   // constant: a unit's pixels are loaded two units ahead (one unit of HBM
   // latency cover instead of one spatial phase).
   uint32_t raw[2][PPL][3];
   unsigned rok[2] = {0u, 0u}, rsh[2] = {0u, 0u};
+  // unit-independent piece geometry, once: hy | hx << 4 | pc << 8 | f << 9,
+  // bit 13 = a piece at all (p < NPC); and its cell slot
+  int pgeo[PPL], pslot[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int p = tid + 512 * j;
+    const int f = p / (2 * CH * CW), r1 = p - f * (2 * CH * CW);
+    const int pc = r1 / (CH * CW), r2 = r1 - pc * (CH * CW), hy = r2 / CW, hx = r2 - hy * CW;
+    pgeo[j] = p < NPC ? hy | (hx << 4) | (pc << 8) | (f << 9) | (1 << 13) : 0;
+    pslot[j] = f * FSL + pc * PP + hy * RPX + hx;
+  }
   auto load_raw = [&](auto setc, int u) {
     constexpr int SET = decltype(setc)::value;
     const int n = u / BPC, b = u - n * BPC;
     const int y0 = (b / BPR) * BH, x0 = (b - (b / BPR) * BPR) * BW;
     rok[SET] = 0u;
     rsh[SET] = 0u;
+    const size_t cb = (size_t)(n * 3) * T_IN * H * W;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
-      const int p = tid + 512 * j;
-      const int f = p / (2 * CH * CW), r1 = p - f * (2 * CH * CW);
-      const int pc = r1 / (CH * CW), r2 = r1 - pc * (CH * CW), hy = r2 / CW, hx = r2 - hy * CW;
+      const int gq = pgeo[j];
+      const int hy = gq & 15, hx = (gq >> 4) & 15, pc = (gq >> 8) & 1, f = (gq >> 9) & 15;
       const int Y = y0 + hy, X = x0 + hx, y = 2 * (Y - pb) + pc, x = 2 * (X - pb);
-      const bool ok = p < NPC && Y >= pb && X >= pb && y < H && x < W;
-      const size_t off = ok ? ((size_t)(n * 3) * T_IN + f) * H * W + (size_t)y * W + x : 0;
+      const bool ok = (gq >> 13) && Y >= pb && X >= pb && y < H && x < W;
+      const size_t off = ok ? cb + (size_t)(f * H + y) * W + x : 0;
       rok[SET] |= ok ? 1u << j : 0u;
       rsh[SET] |= ((unsigned)(off >> 1) & 1u) << j;
 #pragma unroll
@@ -1438,10 +1456,7 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
     constexpr int SET = decltype(setc)::value;
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
-      const int p = tid + 512 * j;
-      if (p < NPC) {
-        const int f = p / (2 * CH * CW), r1 = p - f * (2 * CH * CW);
-        const int pc = r1 / (CH * CW), r2 = r1 - pc * (CH * CW), hy = r2 / CW, hx = r2 - hy * CW;
+      if (pgeo[j] >> 13) {
         const bool ok = (rok[SET] >> j) & 1u;
         const unsigned sh = ((rsh[SET] >> j) & 1u) * 16u;
         u16x8 v;
@@ -1454,7 +1469,7 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
         }
         v[3] = 0;
         v[7] = 0;
-        *(u16x8*)(cells + ((f * 2 + pc) * CH * RPX + hy * RPX + hx) * 8) = v;
+        *(u16x8*)(cells + pslot[j] * 8) = v;
       }
     }
   };
@@ -1462,7 +1477,7 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
   // spatial fragment offsets: lane (g, r16) = position (py, px) of the box,
   // piece g & 1 of the cell at tap column offset g >> 1 (conv_s2d4)
   const int py = r16 >> 3, px = r16 & 7;
-  const int cbo = ((g & 1) * CH + py) * RPX + px + (g >> 1);
+  const int cbo = (g & 1) * PP + py * RPX + px + (g >> 1);
   // S image: chunk c, frame d, position r16, channel piece q at ((c * 16 + d) * 16 + r16) * 32 + ((q ^ ((r16 >> 1) & 2)) << 3)
   const int rdoff = r16 * 32 + ((g ^ ((r16 >> 1) & 2)) << 3);
   const int fp = wave & 3, hh = wave >> 2;
@@ -1486,9 +1501,6 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
     using SQ = std::integral_constant<int, P ^ 1>;
     const int un = u + G;
     B0_STAMP(0);
-    // (past the end: a dummy load of unit 0, so the compiler's wait counts
-    // are the same on every path)
-    load_raw(SP{}, u + 2 * G < nunits ? u + 2 * G : 0);
     // A: cells of u written, the S image free.  The three phase barriers
     // order LDS only (no global data passes between waves): lgkmcnt +
     // s_barrier, not __syncthreads, whose fence would also wait for the
@@ -1514,10 +1526,16 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
         for (int ct = 0; ct < 4; ++ct) sacc[fi][ct] = T::mfma(wf[ct], pf, sacc[fi][ct]);
       }
     }
+    // the pixels of the unit after next, issued behind the spatial MFMAs (past
+    // the end: a dummy load of unit 0, so the compiler's wait counts are the
+    // same on every path)
+    load_raw(SP{}, u + 2 * G < nunits ? u + 2 * G : 0);
     B0_STAMP(2);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // B: every wave is done with the cells
+    // ---- B: this wave's frames of the S image (bias + ReLU, 16-bit), right
+    // behind its own MFMAs: the previous unit's temporal reads of S ended
+    // before barrier A, and the cells it no longer reads are rewritten only
+    // after barrier C
     B0_STAMP(3);
-    // ---- B: S image (bias + ReLU, 16-bit) and the next unit's cells
 #pragma unroll
     for (int fi = 0; fi < 2; ++fi) {
       const int d = 2 * wave + fi;
@@ -1537,13 +1555,6 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
         *(u16x8*)(simg + (c * T_IN + d) * 512 + rdoff) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
       }
     }
-    // the next unit's pixels (set P^1, loaded one unit ago) have landed: at
-    // most this unit's PPL x 3 loads and the previous unit's 2 output stores
-    // are younger (an intrinsic, not asm, so the compiler's own wait
-    // bookkeeping sees it and adds no vmcnt(0) of its own)
-    static_assert(3 * PPL + 2 < 16, "vmcnt immediate");
-    __builtin_amdgcn_s_waitcnt(0x0F70 | (3 * PPL + 2));
-    if (un < nunits) store_cells(SQ{});
     B0_STAMP(4);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // C: the S image is complete
     B0_STAMP(5);
@@ -1575,6 +1586,15 @@ __global__ __launch_bounds__(512, 1) void s3d_base0(const uint8_t* __restrict__ 
           }
         }
     }
+    // the next unit's cells (the cell image is free since barrier B), here
+    // behind the temporal MFMAs rather than in phase B, where nothing hid
+    // them: its pixels (set P^1, loaded one unit ago) have landed -- at most
+    // this unit's PPL x 3 loads and the previous unit's 2 output stores are
+    // younger (an intrinsic, not asm, so the compiler's own wait bookkeeping
+    // sees it and adds no vmcnt(0) of its own)
+    static_assert(3 * PPL + 2 < 16, "vmcnt immediate");
+    __builtin_amdgcn_s_waitcnt(0x0F70 | (3 * PPL + 2));
+    if (un < nunits) store_cells(SQ{});
     B0_STAMP(6);
     const int n = u / BPC, b = u - n * BPC;
     const int oy = (b / BPR) * BH + py, ox = (b - (b / BPR) * BPR) * BW + px;
