@@ -207,7 +207,11 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * bit-identical outputs), "wino" (bit mask: the 3x3 convs at 14x14 (bit 0),
  * 28x28 (bit 1), 56x56 (bit 2) run as fused Winograd F(2,3) kernels; default
  * 0; NOT bit-identical: a different rounding).  Process-wide knobs of the fac_ops.h layer kernels
- * (A/B measurements; any context sets them): "gemm_small" (the GEMM tile
+ * (A/B measurements; any context sets them): "conv_ring9" (0..7, bit mask of
+ * the conv kernels that take a 9-slice weight ring when the grid is at most 2
+ * workgroups per CU, i.e. few crops: bits 0 and 1 the two 9-slice variants
+ * of the 14x14 BN-64 tile (bit 1 wins), bit 2 the 28x28 conv3x3_db register
+ * ring; default 6; 0 = never; bit-identical outputs), "gemm_small" (the GEMM tile
  * variant 0..6 of calls with <= 64 rows, i.e. forwards of <= 32 crops; default
  * 5, a 64x32 tile; -1 = the wide tiles; every variant gives bit-identical
  * results), "nd_pt_wide" (n >= 0: convnd_pt
