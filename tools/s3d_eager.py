@@ -23,7 +23,18 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--u8", action="store_true", help="uint8 clips (decoded frames: base.0 as one launch)")
     ap.add_argument("--no-fuse", action="store_true", help="with --u8: base.0 as two launches")
+    ap.add_argument("--opt", action="append", default=[], help="process-wide fac_set_option knob, name=value")
     a = ap.parse_args()
+    if a.opt:
+        import ctypes
+        from fac_fake_amd import _lib
+        lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(lib.fac_create(0, _lib.DTYPES[a.dtype], ctypes.byref(h)), None, "fac_create")
+        for kv in a.opt:
+            k, v = kv.split("=")
+            _lib.check(lib.fac_set_option(h, k.encode(), int(v)), h, "fac_set_option")
+        lib.fac_destroy(h)
     dev = torch.device("cuda:0")
     m = S3D(1, "no", dtype=a.dtype)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, False).items()})
