@@ -169,7 +169,18 @@ def check_function(name: str, code: list, rep: Report) -> None:
                 if len(lg) < L:
                     rep.problems.append(f"{name} @0x{ins.addr:x}: only {len(lg)} LGKM ops since the previous "
                                         f"barrier, lgkmcnt({L})")
-                for r in lg[len(lg) - L:]:
+                # the LGKM ops still in flight at the barrier: replay the
+                # step's own lgkmcnt waits (each leaves only its k youngest
+                # outstanding), then the barrier's lgkmcnt(L)
+                pend = []
+                for s in seg:
+                    if _is_lgkm(s.op):
+                        pend.append(s)
+                    else:
+                        k = _lgkm_wait(s)
+                        if k is not None:
+                            pend = pend[len(pend) - k:] if k else []
+                for r in pend[max(0, len(pend) - L):]:
                     if r.op != "ds_read_b128":
                         rep.problems.append(f"{name} @0x{r.addr:x}: {r.op} among the {L} LDS ops left in flight")
                         continue

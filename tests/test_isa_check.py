@@ -52,6 +52,19 @@ def test_ring_read_left_in_flight_is_caught():
     assert not rep.ok and any("not an MFMA A operand" in p for p in rep.problems)
 
 
+def test_ring_read_retired_by_a_step_wait_passes():
+    # the B read sits among the last reads in program order, but a
+    # lgkmcnt(0) inside the step retires it: only the A prefetch behind that
+    # wait is in flight at the barrier (the compiler's order in the round-5
+    # chunk-planar 112^2 tiles)
+    step = ["ds_read_b128 v[46:49], v72 offset:16", "ds_read_b128 v[50:53], v90 offset:59392",
+            "s_waitcnt lgkmcnt(0)",
+            "v_mfma_f32_16x16x32_bf16 v[2:5], v[46:49], v[50:53], v[2:5]",
+            "ds_read_b128 v[42:45], v96 offset:16"]
+    rep = _check(["s_barrier"] + step + ["s_waitcnt lgkmcnt(2)"] + NEXT)
+    assert rep.waits == 1 and rep.ok, rep.problems
+
+
 def test_scalar_load_in_step_is_caught():
     rep = _check(["s_barrier", "s_load_dwordx4 s[4:7], s[0:1], 0x10"] + STEP + ["s_waitcnt lgkmcnt(2)"] + NEXT)
     assert not rep.ok and any("scalar-memory" in p for p in rep.problems)
