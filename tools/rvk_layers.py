@@ -3,7 +3,7 @@
 layer's median event-timed duration over a few eager forwards, with its
 algorithmic TFLOP/s and minimum HBM GB/s.  GPU box only.
 
-    python tools/rvk_layers.py [--model rvk|s3d] [--B 256] [--dtype bf16]
+    python tools/rvk_layers.py [--model rvk|s3d] [--B 256] [--dtype bf16] [--u8]
 """
 import argparse
 import sys
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--B", type=int, default=0)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--u8", action="store_true", help="S3D: uint8 clips (decoded frames; base.0 as one launch)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     if a.model == "rvk":
@@ -41,6 +42,8 @@ def main():
         m = S3D(1, "no", dtype=a.dtype)
         m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in make_s3d_state_dict(0, 1, False).items()})
         clips = torch.from_numpy(s3d_clips(a.B, 16, 112, seed=3)).to(dev)
+        if a.u8:
+            clips = clips.to(torch.uint8)
         run = lambda: m(clips)  # noqa: E731
     run()
     torch.cuda.synchronize()
