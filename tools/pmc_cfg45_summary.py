@@ -1,4 +1,4 @@
-"""Summarise tools/archive/pmc_cfg45_r03.sh's passes into one JSON per model.
+"""Summarise tools/pmc_cfg45.sh's passes into one JSON per model.
 
     python tools/pmc_cfg45_summary.py gpurun_out/pmc_cfg45h profiles/r03h
 
@@ -58,7 +58,7 @@ def summarise(src: Path, model: str, forwards: int) -> dict:
     if tot.get("FETCH_SIZE"):
         res["forward"]["hbm_bytes_per_forward"] = round((2 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0 / forwards)
     res["forwards_profiled"] = forwards
-    res["method"] = ("rocprofv3 --pmc, one run per pass (tools/archive/pmc_cfg45_r03.sh) over the eager forwards of "
+    res["method"] = ("rocprofv3 --pmc, one run per pass (tools/pmc_cfg45.sh) over the eager forwards of "
                      "tools/rvk_layers.py; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8)")
     return res
 
