@@ -627,7 +627,7 @@ def main():
     dev = torch.device("cuda", local)
     B = args.batch
     if args.only and args.opt:
-        # process-wide knobs (conv_db, conv_wr, pool_impl) for the sub-measurement A/Bs
+        # process-wide knobs (fac_set_option, e.g. nd_pt_wide, pool_roll) for the sub-measurement A/Bs
         from fac_fake_amd.cvit import CViT
         knobs = CViT(dtype=args.dtype)
         knobs.reserve(1, dev)
