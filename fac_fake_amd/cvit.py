@@ -293,6 +293,8 @@ class CViT(nn.Module):
         pidx = self._pos_index(B, pos_index, x.device)
         logits = torch.empty(B, 2, dtype=torch.float32, device=x.device)
         probs = torch.empty(B, 2, dtype=torch.float32, device=x.device) if want_probs else None
+        if B == 0:  # an empty batch: empty outputs, as the reference's forward gives (the C ABI takes B >= 1)
+            return logits, probs
         stream = torch.cuda.current_stream(x.device).cuda_stream
         fn = lib.fac_forward_nhwc_u8 if u8 else lib.fac_forward_nchw_f32
         args = (self._ctx, x.data_ptr(), B, pidx.data_ptr(), logits.data_ptr(),

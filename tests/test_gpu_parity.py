@@ -256,6 +256,10 @@ def test_ragged_batches_and_edge_sizes(models, golden):
     for B in (1, 2, 3, 17, 31):
         lg = _run_u8(m, crops[:B], np.arange(B))
         assert np.abs(_sig(lg) - _sig(g["logits"][:B])).max() <= 1e-3, B
+    # an empty batch gives empty outputs, as the reference's forward does
+    e = m.forward_u8(torch.from_numpy(crops[:0]).to(DEV), return_probs=True)
+    assert tuple(e[0].shape) == (0, 2) and tuple(e[1].shape) == (0, 2)
+    assert tuple(m(torch.zeros(0, 3, 224, 224, device=DEV)).shape) == (0, 2)
 
 
 def test_reference_forward_contract(models):
