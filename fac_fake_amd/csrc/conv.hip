@@ -913,6 +913,12 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
       if (launch_box<T, 14, 14, 192, 1, 4, 2, 2, false, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)
         return hipErrorInvalidValue;
       break;
+    case 14032:
+      if (ring9 & 2)
+        launch_box<T, 14, 14, 32, 4, 1, 2, 2, true, true, 9>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      else
+        launch_box<T, 14, 14, 32, 4, 1, 2, 2, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+      break;
     case 14064:
       if (ring9 & 2)
         launch_box<T, 14, 14, 64, 1, 4, 2, 2, true, true, 9>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);

@@ -86,6 +86,7 @@ struct ConvLayer {
   // reference's one-video call); bit-identical outputs
   int bn_small = 0;
   uint16_t* w_small = nullptr;
+  uint16_t* w_small32 = nullptr;  // the 14^2 layers packed for 32-channel blocks (option "conv_small14")
   // the 56^2 / 28^2 / 14^2 layers also packed for conv3x3_wino (Winograd F(2,3), wino.hip)
   uint16_t* w_wino = nullptr;
 };
@@ -211,6 +212,7 @@ struct fac_ctx {
   static constexpr int kDirectGraphs = 8;
   int graph_max_b = 32;
   int conv_small = 1;  // option "conv_small": 28^2 / 14^2 layers on half-width column blocks when few crops
+  int small14 = 1;  // option "conv_small14": few-crop 14^2 convs on 32-channel blocks when they fit one per CU (1) or never (0)
   int wino = 0;        // option "wino": bit 0 / 1 / 2 = the 14^2 / 28^2 / 56^2 layers as Winograd F(2,3)
   std::vector<SmallGraph> graphs;
   hipStream_t cap_st = nullptr;
@@ -262,6 +264,13 @@ hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, ui
   const int wbit = L.H == 14 ? 1 : (L.H == 28 ? 2 : (L.H == 56 ? 4 : 0));
   if (L.w_wino && (c->wino & wbit))
     return launch_conv3x3_wino(c->dtype, in, L.w_wino, L.b, out, B, L.H, L.Cin, L.Cout, 64, L.pool, c->zero16, st);
+  // the 14^2 layers on 32-channel blocks while that grid still fits one
+  // workgroup per CU (B <= 16 crops for cout 512): at B = 1 / 8 the graph
+  // forward 0.438 / 0.484 -> 0.419 / 0.465 ms; at B = 29 (464 workgroups)
+  // the 64-channel blocks stay faster (0.655-0.669 vs 0.666-0.676 ms)
+  if (L.w_small32 && c->conv_small && c->small14 && (long long)B * (L.Cout / 32) <= c->num_cu)
+    return launch_conv3x3(c->dtype, in, L.w_small32, L.b, out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st, true,
+                          32);
   if (L.w_small && c->conv_small) {
     const int bn = conv_block_n(L.H, L.Cout), boxes = L.H == 14 ? 1 : (L.H / 4) * (L.H / 28);
     if ((long long)B * boxes * (L.Cout / bn) < c->num_cu)
@@ -472,6 +481,11 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
       if (L.bn_small) {
         fac::pack_conv3x3(c->dtype, H, ci, co, wfold.data(), pk.data(), L.bn_small);
         if ((rc = upload(c, pk, &L.w_small))) return rc;
+      }
+      L.w_small32 = nullptr;
+      if (H == 14) {
+        fac::pack_conv3x3(c->dtype, H, ci, co, wfold.data(), pk.data(), 32);
+        if ((rc = upload(c, pk, &L.w_small32))) return rc;
       }
       L.w_wino = nullptr;
       if (H <= 56) {
@@ -982,6 +996,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "wino") {
     if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "wino must be 0..7 (bit 0: 14^2, 1: 28^2, 2: 56^2)");
     c->wino = value;
+    return FAC_OK;
+  }
+  if (k == "conv_small14") {
+    c->small14 = value != 0;
     return FAC_OK;
   }
   if (k == "conv_small") {

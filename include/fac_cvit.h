@@ -204,7 +204,9 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * fac_forward_nhwc_u8; default 32, 0 = always eager), "conv_small" (1 = the
  * 28x28 / 14x14 convs run on half-width output-channel blocks when the
  * default grid would leave CUs idle, i.e. few crops; the default; 0 = never;
- * bit-identical outputs), "wino" (bit mask: the 3x3 convs at 14x14 (bit 0),
+ * bit-identical outputs), "conv_small14" (1 = with conv_small, the 14x14 convs
+ * on 32-channel blocks while that grid fits one workgroup per CU, i.e. <= 16
+ * crops; the default; 0 = the 64-channel blocks only; bit-identical), "wino" (bit mask: the 3x3 convs at 14x14 (bit 0),
  * 28x28 (bit 1), 56x56 (bit 2) run as fused Winograd F(2,3) kernels; default
  * 0; NOT bit-identical: a different rounding).  Process-wide knobs of the fac_ops.h layer kernels
  * (A/B measurements; any context sets them): "conv_ring9" (0..7, bit mask of

@@ -927,6 +927,37 @@ def test_ring9_conv_is_bit_identical(models, B):
         assert torch.equal(outs[0][1], outs[v][1]), v
 
 
+@pytest.mark.parametrize("B", [5, 16])
+def test_conv_small14_blocks_are_bit_identical(models, B):
+    """Option conv_small14 (the few-crop 14^2 convs on 32-channel blocks while
+    they fit one workgroup per CU: twice the workgroups of the 64-channel
+    ones) only changes which workgroup computes which channels: conv14-17's
+    outputs and the logits are bit-identical to the 64-channel blocks."""
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    m = models["fp16"]
+    x = torch.from_numpy(make_crops(B, seed=83)).to(DEV)
+    pidx = (torch.arange(B) % 32).to(torch.int32)
+    outs = {}
+    try:
+        for v in (0, 1):
+            m.set_option("conv_small14", v)
+            feats = []
+            for layer, shape in ((13, (B, 14, 14, 512)), (14, (B, 14, 14, 512)), (16, (B, 7, 7, 512))):
+                f = torch.empty(*shape, dtype=torch.float16, device=DEV)
+                _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), B, layer, f.data_ptr(), None), m._ctx, "dbg")
+                feats.append(f.view(torch.int16).cpu())
+            lg = m.forward_u8(x, pos_index=pidx)
+            lg2 = m.forward_u8(x, pos_index=pidx)
+            torch.cuda.synchronize()
+            outs[v] = (feats, lg.cpu(), lg2.cpu())
+    finally:
+        m.set_option("conv_small14", 1)
+    for a, b in zip(outs[0][0], outs[1][0]):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+
+
 def test_direct_graph_follows_buffer_contents(models):
     """Small forwards on the same buffers as the previous call replay a graph
     captured on those buffers (no copies): each replay reads the crops the
