@@ -514,12 +514,13 @@ def spawn_ranks(n: int) -> int:
     the JSON line.  If a rank fails the others are terminated; returns the
     first non-zero exit code (0 when every rank succeeded)."""
     import subprocess
-    gloo = os.environ.get("FAC_DIST_BACKEND", "nccl") != "nccl"
-    if not gloo:
-        have = torch.cuda.device_count()
-        if have < n:
-            print(f"[bench] --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
-            return 2
+    # The parent never initialises the GPU (VERDICT r05 item 7): the device
+    # count is checked by each rank (main, before set_device), and this guard
+    # makes any future GPU touch here fail before a child is started.
+    if torch.cuda.is_initialized():
+        raise RuntimeError("bench.py spawn_ranks: the parent process initialised the GPU; refusing to start ranks")
+    print(f"[bench] spawn_ranks parent pid {os.getpid()}: cuda_initialized={torch.cuda.is_initialized()}",
+          file=sys.stderr, flush=True)
     port = _free_port()
     procs = []
     for r in range(n):
@@ -562,8 +563,9 @@ def launch_info(backend: str, world: int, rank: int, local: int) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1,
-                    help="ranks (one per GPU); without torchrun's WORLD_SIZE the script spawns them itself")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU; default 1, or WORLD_SIZE under an external launcher); without "
+                         "torchrun's WORLD_SIZE the script spawns them itself")
     ap.add_argument("--dist-check", action="store_true",
                     help="launch + rendezvous + rank all-gather only, no measurement (the N>1 launcher's CPU test "
                          "with FAC_DIST_BACKEND=gloo)")
@@ -594,12 +596,14 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         # no launcher: start the N ranks here, before anything touches the GPU
         sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is None:       # `torchrun --nproc-per-node N bench.py`: the launcher's world size
+        args.gpus = world
     if world != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
     # RCCL over xGMI; FAC_DIST_BACKEND=gloo only to rehearse the multi-rank
@@ -610,6 +614,9 @@ def main():
         local %= max(torch.cuda.device_count(), 1)   # rehearsal: several ranks may share a GPU
     if world > 1:
         if backend == "nccl":
+            have = torch.cuda.device_count()
+            if have <= local:
+                raise SystemExit(f"[bench] rank {rank}: --gpus {args.gpus} but only {have} GPU(s) visible")
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -22,6 +23,7 @@
 
 namespace fac {
 void set_conv_ring9(int v);
+void set_conv14_grid(int v);
 int conv_block_n(int H, int cout);
 void set_nd_pt_wide(int v);
 void set_gemm_small(int max_m, int variant);
@@ -32,10 +34,6 @@ void set_pool3_zg(int v);
 void set_pool_lds14(int v);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out, int bn = 0);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
-void pack_conv3x3_wino(int dtype, int ci, int co, int bn, const float* w, uint16_t* out);
-hipError_t launch_conv3x3_wino(int dtype, const uint16_t* in, const uint16_t* upk, const float* bias, uint16_t* out,
-                               int B, int H, int Cin, int Cout, int bn, bool pool, const uint16_t* zero16,
-                               hipStream_t st);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, bool relu = true,
                           int bn = 0);
@@ -87,8 +85,6 @@ struct ConvLayer {
   int bn_small = 0;
   uint16_t* w_small = nullptr;
   uint16_t* w_small32 = nullptr;  // the 14^2 layers packed for 32-channel blocks (option "conv_small14")
-  // the 56^2 / 28^2 / 14^2 layers also packed for conv3x3_wino (Winograd F(2,3), wino.hip)
-  uint16_t* w_wino = nullptr;
 };
 
 struct TLayer {
@@ -209,11 +205,11 @@ struct fac_ctx {
   };
   std::vector<LastCall> last_calls;
   unsigned long long graph_clock = 0;
+  unsigned knob_gen = 0;  // g_knob_gen when this context's graphs were (last) known current
   static constexpr int kDirectGraphs = 8;
   int graph_max_b = 32;
   int conv_small = 1;  // option "conv_small": 28^2 / 14^2 layers on half-width column blocks when few crops
   int small14 = 1;  // option "conv_small14": few-crop 14^2 convs on 32-channel blocks when they fit one per CU (1) or never (0)
-  int wino = 0;        // option "wino": bit 0 / 1 / 2 = the 14^2 / 28^2 / 56^2 layers as Winograd F(2,3)
   std::vector<SmallGraph> graphs;
   hipStream_t cap_st = nullptr;
   void* g_in[2] = {nullptr, nullptr};  // [0] fp32 NCHW, [1] uint8 NHWC; graph_max_b crops each
@@ -223,6 +219,13 @@ struct fac_ctx {
 };
 
 namespace {
+
+// Bumped by every fac_set_option call: several knobs are process-wide (they
+// pick kernels for every context), so a graph another context captured before
+// the change would keep the old kernels; forward_graph drops its context's
+// graphs when the generation moved.  Graphs a caller captured
+// around fac_* calls itself (torch.cuda.graph) are the caller's to recapture.
+std::atomic<unsigned> g_knob_gen{0};
 
 int set_err(fac_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -261,9 +264,6 @@ int patch_splits(int) { return kPatchSplits; }
 
 hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, uint16_t* out, int B, hipStream_t st) {
   using namespace fac;
-  const int wbit = L.H == 14 ? 1 : (L.H == 28 ? 2 : (L.H == 56 ? 4 : 0));
-  if (L.w_wino && (c->wino & wbit))
-    return launch_conv3x3_wino(c->dtype, in, L.w_wino, L.b, out, B, L.H, L.Cin, L.Cout, 64, L.pool, c->zero16, st);
   // the 14^2 layers on 32-channel blocks while that grid still fits one
   // workgroup per CU (B <= 16 crops for cout 512): at B = 1 / 8 the graph
   // forward 0.438 / 0.484 -> 0.419 / 0.465 ms; at B = 29 (464 workgroups)
@@ -486,12 +486,6 @@ int load_impl(fac_ctx* c, const fac_tensor_desc* descs, int n) {
       if (H == 14) {
         fac::pack_conv3x3(c->dtype, H, ci, co, wfold.data(), pk.data(), 32);
         if ((rc = upload(c, pk, &L.w_small32))) return rc;
-      }
-      L.w_wino = nullptr;
-      if (H <= 56) {
-        std::vector<uint16_t> pw((size_t)co * ci * 12);
-        fac::pack_conv3x3_wino(c->dtype, ci, co, 64, wfold.data(), pw.data());
-        if ((rc = upload(c, pw, &L.w_wino))) return rc;
       }
       if ((rc = upload(c, bf, &L.b))) return rc;
     }
@@ -820,6 +814,10 @@ int forward_graph(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pid
   DevGuard g(c->device);
   int rc = ensure_ws(c, B);
   if (rc) return rc;
+  if (const unsigned gen = g_knob_gen.load(); gen != c->knob_gen) {
+    drop_graphs(c);  // a process-wide knob changed since these were captured
+    c->knob_gen = gen;
+  }
   const int kind = (u8 ? 1 : 0) | (probs ? 2 : 0);
   ++c->graph_clock;
   // direct graph for these buffers?
@@ -983,9 +981,11 @@ int fac_set_stem_chunk(fac_ctx* c, int crops) {
 int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (!c || !key) return FAC_ERR_ARG;
   const std::string k(key);
-  {  // every knob can change what a captured forward would launch
+  {  // every knob can change what a captured forward would launch -- in this
+     // context, and for the process-wide ones in every other (g_knob_gen)
     DevGuard g(c->device);
     drop_graphs(c);
+    c->knob_gen = ++g_knob_gen;
   }
   if (k == "stem_chunk") return fac_set_stem_chunk(c, value);
   if (k == "conv_ring9") {  // process-wide A/B: 9-slice weight ring (bit 0: the 14x14 / BN 64 tile)
@@ -993,9 +993,9 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     fac::set_conv_ring9(value);
     return FAC_OK;
   }
-  if (k == "wino") {
-    if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "wino must be 0..7 (bit 0: 14^2, 1: 28^2, 2: 56^2)");
-    c->wino = value;
+  if (k == "conv14_grid") {  // process-wide A/B: wave grid of the 14x14 / BN 128 conv tile (conv.hip)
+    if (value < 0 || value > 4) return set_err(c, FAC_ERR_ARG, "conv14_grid must be 0..4");
+    fac::set_conv14_grid(value);
     return FAC_OK;
   }
   if (k == "conv_small14") {

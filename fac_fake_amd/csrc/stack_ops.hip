@@ -22,11 +22,6 @@ int conv_block_n(int H, int cout);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
                           int B, int H, int W, int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st,
                           bool relu, int bn = 0);
-void pack_conv3x3_wino(int dtype, int ci, int co, int bn, const float* w, uint16_t* out);
-size_t wino_packed_elems(int ci, int co);
-hipError_t launch_conv3x3_wino(int dtype, const uint16_t* in, const uint16_t* upk, const float* bias, uint16_t* out,
-                               int B, int H, int Cin, int Cout, int bn, bool pool, const uint16_t* zero16,
-                               hipStream_t st);
 hipError_t launch_stem224(int dtype, bool u8, const void* in, const uint16_t* w1, const float* b1, const uint16_t* w2,
                           const float* b2, const uint16_t* w3, const float* b3, uint16_t* out, int B, int nwg,
                           hipStream_t s);
@@ -108,27 +103,6 @@ int fac_conv3x3(int dtype, const void* in, const void* wpk, const float* bias, v
   const hipError_t e = fac::launch_conv3x3(dtype, (const uint16_t*)in, (const uint16_t*)wpk, bias, (uint16_t*)out, n,
                                            h, h, cin, cout, pool != 0, (const uint16_t*)zero256,
                                            (hipStream_t)stream, relu != 0);
-  return e == hipSuccess ? FAC_OK : FAC_ERR_HIP;
-}
-
-size_t fac_conv3x3_wino_packed_elems(int cin, int cout) {
-  return cin >= 32 && cin % 32 == 0 && cout >= 64 && cout % 64 == 0 ? fac::wino_packed_elems(cin, cout) : 0;
-}
-
-int fac_conv3x3_wino_pack(int dtype, int cin, int cout, const float* w, uint16_t* out) {
-  if (!w || !out || (dtype != 0 && dtype != 1)) return FAC_ERR_ARG;
-  if (!fac_conv3x3_wino_packed_elems(cin, cout)) return FAC_ERR_SHAPE;
-  fac::pack_conv3x3_wino(dtype, cin, cout, 64, w, out);
-  return FAC_OK;
-}
-
-int fac_conv3x3_wino(int dtype, const void* in, const void* wpk, const float* bias, void* out, int n, int h, int cin,
-                     int cout, int pool, const void* zero256, void* stream) {
-  if (!in || !wpk || !bias || !out || !zero256 || n <= 0 || (dtype != 0 && dtype != 1)) return FAC_ERR_ARG;
-  if (!fac_conv3x3_wino_packed_elems(cin, cout) || (h != 14 && h != 28 && h != 56)) return FAC_ERR_SHAPE;
-  const hipError_t e = fac::launch_conv3x3_wino(dtype, (const uint16_t*)in, (const uint16_t*)wpk, bias, (uint16_t*)out,
-                                                n, h, cin, cout, 64, pool != 0, (const uint16_t*)zero256,
-                                                (hipStream_t)stream);
   return e == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 

@@ -78,12 +78,23 @@ def weight_versions(module: nn.Module) -> tuple:
     in-place update or a swapped tensor changes this.  The (module, name)
     slots are listed once; walking them costs ~40-70 us per call, against
     ~0.5 ms for the state_dict() this replaced (it ran on every forward, the
-    reference's one-video call included)."""
-    slots = module.__dict__.get("_wv_slots")
-    if slots is None:
-        slots = [(m._parameters, k) for _, m in module.named_modules() for k in m._parameters] + \
-                [(m._buffers, k) for _, m in module.named_modules() for k in m._buffers]
-        module.__dict__["_wv_slots"] = slots
+    reference's one-video call included).  The cached slots are rebuilt when
+    the module tree changed since they were listed (a submodule replaced,
+    added or removed, e.g. ``m.mlp_head[2] = nn.Linear(...)``): each module's
+    children are compared by identity, ~10 us."""
+    cache = module.__dict__.get("_wv_slots")
+    if cache is not None:
+        for kids, seen in cache[0]:
+            if len(kids) != len(seen) or any(a is not b for a, b in zip(kids.values(), seen)):
+                cache = None
+                break
+    if cache is None:
+        mods = [m for _, m in module.named_modules()]
+        tree = [(m._modules, tuple(m._modules.values())) for m in mods]
+        slots = [(m._parameters, k) for m in mods for k in m._parameters] + \
+                [(m._buffers, k) for m in mods for k in m._buffers]
+        cache = module.__dict__["_wv_slots"] = (tree, slots)
+    slots = cache[1]
     out = []
     for d, k in slots:
         t = d[k]

@@ -206,10 +206,13 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * default grid would leave CUs idle, i.e. few crops; the default; 0 = never;
  * bit-identical outputs), "conv_small14" (1 = with conv_small, the 14x14 convs
  * on 32-channel blocks while that grid fits one workgroup per CU, i.e. <= 16
- * crops; the default; 0 = the 64-channel blocks only; bit-identical), "wino" (bit mask: the 3x3 convs at 14x14 (bit 0),
- * 28x28 (bit 1), 56x56 (bit 2) run as fused Winograd F(2,3) kernels; default
- * 0; NOT bit-identical: a different rounding).  Process-wide knobs of the fac_ops.h layer kernels
- * (A/B measurements; any context sets them): "conv_ring9" (0..7, bit mask of
+ * crops; the default; 0 = the 64-channel blocks only; bit-identical).
+ * Process-wide knobs of the fac_ops.h layer kernels (A/B measurements; any
+ * context sets them; every fac_set_option call makes every context recapture
+ * its small-batch graphs before their next replay): "conv14_grid" (wave grid
+ * of the 14x14 / BN-128 conv tile: 0 = 1 x 4, 1 = 2 x 2, 2 = 2 x 2 with the
+ * padding row tile skipped, 3 = 2 with the B-fragment prefetch, 4 = 1 with
+ * it; bit-identical outputs), "conv_ring9" (0..7, bit mask of
  * the conv kernels that take a 9-slice weight ring when the grid is at most 2
  * workgroups per CU, i.e. few crops: bits 0 and 1 the two 9-slice variants
  * of the 14x14 BN-64 tile (bit 1 wins), bit 2 the 28x28 conv3x3_db register

@@ -233,19 +233,6 @@ int fac_conv3x3_pack(int dtype, int h, int cin, int cout, const float* w, uint16
 int fac_conv3x3(int dtype, const void* in, const void* wpk, const float* bias, void* out, int n, int h, int cin,
                 int cout, int pool, int relu, const void* zero256, void* stream);
 
-/* The same conv (+ folded BN + ReLU, + MaxPool2d(2,2) if pool) as Winograd
- * F(2,3) along x (wino.hip): per output pair the four transformed inputs
- * d0-d2, d1+d2, d2-d1, d1-d3 are rounded to 16 bits, multiplied by the
- * transformed kernel rows g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2 (rounded to 16
- * bits once, at packing), accumulated in fp32 and recombined in fp32: 2/3 of
- * the direct conv's MFMA work.  h in {14, 28, 56}, cin a multiple of 32, cout
- * a multiple of 64.  wpk: fac_conv3x3_wino_pack of the folded fp32 weight
- * [cout][cin][3][3] (fac_conv3x3_wino_packed_elems 16-bit elements). */
-size_t fac_conv3x3_wino_packed_elems(int cin, int cout);
-int fac_conv3x3_wino_pack(int dtype, int cin, int cout, const float* w, uint16_t* out);
-int fac_conv3x3_wino(int dtype, const void* in, const void* wpk, const float* bias, void* out, int n, int h, int cin,
-                     int cout, int pool, const void* zero256, void* stream);
-
 /* The fused 224x224 block (stem224.hip): input normalisation, conv 3->32,
  * conv 32->32, conv 32->32 (each + folded BN + ReLU), MaxPool2d(2,2) ->
  * [n][112][112][32].  u8: uint8 NHWC crops [n][224][224][3] (x/255 and

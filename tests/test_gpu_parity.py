@@ -816,83 +816,40 @@ def test_few_crop_forward_equals_full_batch(models, dt):
     assert np.array_equal(off, small)
 
 
-WINO_CASES = [(14, 256, 512, 0), (14, 512, 512, 1), (28, 128, 256, 0), (28, 256, 256, 1), (56, 64, 128, 0),
-              (56, 128, 128, 1), (28, 32, 64, 0)]
-
-
-@pytest.mark.parametrize("h,cin,cout,pool", WINO_CASES)
-@pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_wino_conv_vs_emulation(h, cin, cout, pool, dt, torch_threads):
-    """conv3x3_wino (Winograd F(2,3) along x, wino.hip) through the C ABI
-    against the oracle's emulation of its rounding points
-    (oracle.cvit_torch.conv3x3_wino_f23: 16-bit transformed inputs and
-    kernel rows, fp32 sums): up to fp32 summation-order flips of the 16-bit
-    output (<= 2 ulps, a small fraction); against the direct conv of the same
-    operands within the Winograd rounding itself; every 14x14 box of the
-    14 / 28 / 56 maps, image borders, one and many channel chunks, the fused
-    2x2 max-pool, several column blocks."""
+@pytest.mark.parametrize("B", [64, 70])
+def test_conv14_grid_is_bit_identical(models, B):
+    """Option conv14_grid (the wave grid of the 14x14 / BN-128 conv tile: 1 x 4,
+    2 x 2, 2 x 2 skipping the padding row tile, with / without the B-fragment
+    prefetch) only changes which wave computes which (pixel, channel) tiles;
+    each output keeps its k order, so conv14-17's outputs and the logits are
+    bit-identical in both dtypes (B >= 64: the BN-128 grid, not the few-crop
+    blocks; 70: a ragged last XCD range)."""
     from fac_fake_amd import _lib
-    from fac_fake_amd.ops import TORCH16, _zero256
-    from oracle.cvit_torch import conv3x3_wino_f23, round_to
     lib = _lib.load()
-    g = torch.Generator().manual_seed(h * 7 + cin + cout + pool)
-    n = 3
-    x = torch.randn(n, h, h, cin, generator=g).relu().to(TORCH16[dt])
-    w = (torch.randn(cout, cin, 3, 3, generator=g) / np.sqrt(9 * cin)).contiguous()
-    b = torch.randn(cout, generator=g) * 0.1
-    ne = lib.fac_conv3x3_wino_packed_elems(cin, cout)
-    assert ne == cout * cin * 12
-    pk = torch.empty(ne, dtype=torch.int16)
-    _lib.check(lib.fac_conv3x3_wino_pack(_lib.DTYPES[dt], cin, cout, w.data_ptr(), pk.data_ptr()), None, "pack")
-    ho = h // 2 if pool else h
-    y = torch.empty(n, ho, ho, cout, dtype=TORCH16[dt], device=DEV)
-    xd, bd, pkd = x.to(DEV), b.to(DEV), pk.to(DEV)
-    _lib.check(lib.fac_conv3x3_wino(_lib.DTYPES[dt], xd.data_ptr(), pkd.data_ptr(), bd.data_ptr(), y.data_ptr(), n, h,
-                                    cin, cout, pool, _zero256(xd.device).data_ptr(),
-                                    torch.cuda.current_stream().cuda_stream), None, "fac_conv3x3_wino")
-    torch.cuda.synchronize()
-    xin = x.float().permute(0, 3, 1, 2)
-    ref = torch.relu(conv3x3_wino_f23(xin, w, b, dt))
-    direct = torch.relu(torch.nn.functional.conv2d(xin, w, b, padding=1))
-    if pool:
-        ref = torch.nn.functional.max_pool2d(ref, 2)
-        direct = torch.nn.functional.max_pool2d(direct, 2)
-    ref = round_to(ref, dt).permute(0, 2, 3, 1)
-    direct = direct.permute(0, 2, 3, 1)
-    got = y.float().cpu()
-    assert _ulp_diff(got, ref, dt) <= 2.01, _ulp_diff(got, ref, dt)
-    assert float((got != ref).float().mean()) <= 0.05
-    assert _rms_rel(got, direct) <= 4 * ULP_REL[dt]
-
-
-@pytest.mark.parametrize("dt", ["fp16", "bf16"])
-def test_wino_forward_vs_emulation_and_goldens(models, golden, dt, torch_threads):
-    """Option "wino" (the 56^2 / 28^2 / 14^2 convs as Winograd F(2,3)): the
-    whole forward against the oracle's emulation with the same layers as
-    Winograd, and, at fp16, the reference's fp32 goldens within the 1e-3
-    per-frame bar (tools/winograd_budget.py holds the budget)."""
-    from oracle.cvit_torch import forward_emulated, forward_fp32, normalize_u8
-    from fac_fake_amd.weights import make_state_dict
-    m = models[dt]
-    g256 = golden("golden_b256.npz")
-    m.set_option("wino", 7)
-    try:
-        lg = _run_u8(m, make_crops(256, seed=3), np.arange(256) % 32)
-        c4 = make_crops(4, seed=31)
-        lg4 = _run_u8(m, c4, np.arange(4, dtype=np.int32))
-    finally:
-        m.set_option("wino", 0)
-    err = np.abs(_sig(lg.astype(np.float64)) - _sig(g256["logits"].astype(np.float64))).max()
-    if dt == "fp16":
-        assert err <= 1e-3, err
-    # the distance from fp32 is what the Winograd rounding points give (the
-    # emulation with the same layers as Winograd), as test_error_envelope_end_to_end
-    sd = make_state_dict(0)
-    x = normalize_u8(c4)
-    emu = forward_emulated(sd, x, np.arange(4), dt, wino=set(range(6, 17)))
-    fp = forward_fp32(sd, x, np.arange(4))
-    got = torch.from_numpy(lg4)
-    assert _rms_rel(got, fp) <= 1.6 * _rms_rel(emu, fp) + 1e-4, (_rms_rel(got, fp), _rms_rel(emu, fp))
+    x = torch.from_numpy(make_crops(B, seed=91)).to(DEV)
+    pidx = (torch.arange(B) % 32).to(torch.int32)
+    for dt in ("fp16", "bf16"):
+        m = models[dt]
+        tdt = torch.float16 if dt == "fp16" else torch.bfloat16
+        outs = {}
+        try:
+            for v in (0, 1, 2, 3, 4):
+                m.set_option("conv14_grid", v)
+                feats = []
+                for layer, shape in ((13, (B, 14, 14, 512)), (14, (B, 14, 14, 512)), (16, (B, 7, 7, 512))):
+                    f = torch.empty(*shape, dtype=tdt, device=DEV)
+                    _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), B, layer, f.data_ptr(), None), m._ctx,
+                               "dbg")
+                    feats.append(f.view(torch.int16).cpu())
+                lg = m.forward_u8(x, pos_index=pidx)
+                torch.cuda.synchronize()
+                outs[v] = (feats, lg.cpu())
+        finally:
+            m.set_option("conv14_grid", 0)
+        for v in (1, 2, 3, 4):
+            for a, b in zip(outs[0][0], outs[v][0]):
+                assert torch.equal(a, b), (dt, v)
+            assert torch.equal(outs[0][1], outs[v][1]), (dt, v)
 
 
 @pytest.mark.parametrize("B", [3, 29])

@@ -159,6 +159,29 @@ def test_load_state_dict_roundtrip(sd):
         m.load_state_dict({"pos_embedding": torch.zeros(32, 1, 1024)})   # strict, like nn.Module
 
 
+def test_weight_versions_follow_replaced_submodules():
+    """the drop-ins' weight-change check caches its parameter
+    slots; replacing a submodule after the first call (or updating a weight in
+    place, or swapping a tensor) must still change the versions tuple."""
+    from fac_fake_amd.cvit import CViT, weight_versions
+    m = CViT()
+    v0 = weight_versions(m)
+    assert weight_versions(m) == v0
+    head0 = getattr(m.mlp_head, "0")
+    with torch.no_grad():
+        head0.weight.add_(1.0)                                                  # in place
+    v1 = weight_versions(m)
+    assert v1 != v0
+    head0.weight = torch.nn.Parameter(head0.weight.detach().clone())            # swapped tensor
+    v2 = weight_versions(m)
+    assert v2 != v1
+    out_f, in_f = head0.weight.shape
+    setattr(m.mlp_head, "0", torch.nn.Linear(in_f, out_f))                      # replaced submodule
+    v3 = weight_versions(m)
+    assert v3 != v2 and len(v3) == len(v2)
+    assert weight_versions(m) == v3
+
+
 def test_constructor_contract():
     from fac_fake_amd.cvit import CViT
     with pytest.raises(AssertionError):
