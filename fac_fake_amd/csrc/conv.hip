@@ -161,8 +161,10 @@ __device__ unsigned long long conv_st[16384][4][14];
 // WM, e.g. the 14x14 box on 2 x 2 waves: 13 tiles -> 14): the waves of the
 // last wave row skip their one padding tile (its MFMAs and fragment reads),
 // so the box costs 13 tiles of MFMAs, not 14.
+// RES: the image size when it is not the box shape's default (tile_res):
+// the 14x14 boxes also tile the 28x28 layers (option "conv28_grid").
 template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
-          int WR = 3, bool SKIP = false>
+          int WR = 3, bool SKIP = false, int RES = 0>
 __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
@@ -210,8 +212,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   static_assert(CTW * 16 * WN == BN, "BN split");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
-  static_assert(tile_res<TH, TW, BN>() > 0, "tile shape without a resolution");
-  H = W = tile_res<TH, TW, BN>();  // == the launch's H (launch_conv_t); folds the index math
+  static_assert((RES ? RES : tile_res<TH, TW, BN>()) > 0, "tile shape without a resolution");
+  H = W = RES ? RES : tile_res<TH, TW, BN>();  // == the launch's H (launch_conv_t); folds the index math
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
@@ -835,20 +837,20 @@ int conv_block_n(int H, int cout) {
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
 // spill with it; no model pools after such a layer).
 template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true,
-          int WR = 3, bool SKIP = false>
+          int WR = 3, bool SKIP = false, int RES = 0>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if constexpr (POOLED) {
     if (pool) {
-      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, WR, SKIP>
+      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, WR, SKIP, RES>
           <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, WR, SKIP>
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, WR, SKIP, RES>
       <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
@@ -894,6 +896,16 @@ void set_conv_ring9(int v) { g_ring9 = v; }
 // 3 = 2 with the B-fragment prefetch (PB), 4 = 1 with PB
 static int g_conv14_grid = 0;
 void set_conv14_grid(int v) { g_conv14_grid = v; }
+// The 28x28 layers with 128-channel blocks (option "conv28_grid", process-wide,
+// A/B; weights packed for BN 128): 0 = conv3x3_db's 4x28 box (1 x 4 waves,
+// B fragments from L2 per wave: 146 B of L2 reads per MFMA, at the CU's L2
+// fetch rate), 1 = four 14x14 boxes per image on the 2 x 2 LDS-ring tile
+// with the padding tile skipped (the slice is shared by two wave rows and
+// 196 pixels: ~100 B per MFMA), 2 = that tile without the skip, 3 = with
+// the B-fragment prefetch
+static int g_conv28_grid = 0;
+void set_conv28_grid(int v) { g_conv28_grid = v; }
+int conv28_grid() { return g_conv28_grid; }
 static int cu_count() {
   static int cached[64] = {0};
   int dev = 0;
@@ -931,7 +943,18 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
     case 28256: launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28192: launch_db<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28128:
-      if (ring9 & 4)
+      if (g_conv28_grid && !few) {
+        switch (g_conv28_grid) {
+          case 2:
+            launch_box<T, 14, 14, 128, 2, 2, 2, 2, false, true, 3, false, 28>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+            break;
+          case 3:
+            launch_box<T, 14, 14, 128, 2, 2, 2, 2, true, true, 3, false, 28>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+            break;
+          default:
+            launch_box<T, 14, 14, 128, 2, 2, 2, 2, false, true, 3, true, 28>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
+        }
+      } else if (ring9 & 4)
         launch_db<T, 4, 28, 128, 1, 4, 2, 9>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       else
         launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);

@@ -56,6 +56,21 @@ def main():
             torch.cuda.empty_cache()
         out[name] = row
         print(name, json.dumps(row), flush=True)
+    # reference points: a square GEMM (what the library reaches on an easy
+    # shape) and one conv tap as its own GEMM (K = Cin: the nine per-tap
+    # GEMMs of an implicit conv, without the 9x im2col operand)
+    for name, M, N, K in (("square8192", 8192, 8192, 8192), ("conv15_tap", args.B * 196, 512, 512),
+                          ("conv11_tap", args.B * 784, 256, 256)):
+        row = {"M": M, "N": N, "K": K}
+        for dt in (torch.float16, torch.bfloat16):
+            a = torch.randn(M, K, device=dev).to(dt)
+            b = torch.randn(N, K, device=dev).to(dt).t()
+            us = time_mm(a, b)
+            tag = "fp16" if dt == torch.float16 else "bf16"
+            row[tag] = {"us": round(us, 1), "frac": round(2.0 * M * N * K / us / 1e6 / PEAK, 3)}
+            del a, b
+        out[name] = row
+        print(name, json.dumps(row), flush=True)
     print(json.dumps({"gemm_ceiling": out, "B": args.B, "device": torch.cuda.get_device_name(0)}), flush=True)
 
 
