@@ -157,14 +157,8 @@ __device__ unsigned long long conv_st[16384][4][14];
 // slice 0 into dead slots, as with 3).  (Round 5: the 9-slice ring for the 112^2 layers, 61 KB of LDS,
 // i.e. 2 per CU instead of 4, was slower, conv4 161 -> 188 us: there
 // occupancy, not the slice wait, sets the rate.)
-// SKIP (wave grids with WM > 1 whose row tiles were padded to a multiple of
-// WM, e.g. the 14x14 box on 2 x 2 waves: 13 tiles -> 14): the waves of the
-// last wave row skip their one padding tile (its MFMAs and fragment reads),
-// so the box costs 13 tiles of MFMAs, not 14.
-// RES: the image size when it is not the box shape's default (tile_res):
-// the 14x14 boxes also tile the 28x28 layers (option "conv28_grid").
 template <class T, int TH, int TW, int BN, int WM, int WN, bool POOL, int HB = 2, int OCC = 2, bool PB = true,
-          int WR = 3, bool SKIP = false, int RES = 0>
+          int WR = 3>
 __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __restrict__ in,
                                                        const uint16_t* __restrict__ wpk,
                                                        const float* __restrict__ bias,
@@ -179,7 +173,6 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   constexpr int RT = ((NPIX + 15) / 16 + WM - 1) / WM * WM;
   constexpr int RTW = RT / WM;
   constexpr int CTW = BN / 16 / WN;
-  static_assert(!SKIP || (WM > 1 && RT - (NPIX + 15) / 16 == 1), "SKIP: exactly one padding tile, in the last wave row");
   // The halo image is filled by global_load_lds, one 64-slot wave
   // instruction at a time; pad it to whole instructions, a multiple of 4 so
   // every wave issues the same number (HPW).
@@ -212,8 +205,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   static_assert(CTW * 16 * WN == BN, "BN split");
   __shared__ __attribute__((aligned(16))) uint16_t smem[SMEM];
 
-  static_assert((RES ? RES : tile_res<TH, TW, BN>()) > 0, "tile shape without a resolution");
-  H = W = RES ? RES : tile_res<TH, TW, BN>();  // == the launch's H (launch_conv_t); folds the index math
+  static_assert(tile_res<TH, TW, BN>() > 0, "tile shape without a resolution");
+  H = W = tile_res<TH, TW, BN>();  // == the launch's H (launch_conv_t); folds the index math
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int tiles_x = W / TW, tiles_per_img = (H / TH) * tiles_x;
@@ -357,126 +350,113 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_bn_relu(const uint16_t* __re
   // PB: slot 0 is re-filled at step 0, after every wave has read slice 0
   if constexpr (PB) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
-  // NRT: the row tiles this wave computes (RTW, or RTW - 1 with SKIP in the
-  // last wave row: a wave-uniform branch around two copies of the loop)
-  auto mainloop = [&](auto nrt_c) {
-    constexpr int NRT = decltype(nrt_c)::value;
-    for (int c = 0; c < nchunks; ++c) {
-      if constexpr (HB == 1) {
-        if (c > 0) {  // every wave is past the previous chunk's last barrier
-          issue_halo(hbase, c);
-          asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  for (int c = 0; c < nchunks; ++c) {
+    if constexpr (HB == 1) {
+      if (c > 0) {  // every wave is past the previous chunk's last barrier
+        issue_halo(hbase, c);
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
-          for (int rt = 0; rt < NRT; ++rt) fa[rt] = *(const u16x8*)(hbase + abase[rt]);
+        for (int rt = 0; rt < RTW; ++rt) fa[rt] = *(const u16x8*)(hbase + abase[rt]);
+      }
+    }
+    const uint16_t* hb = hbase + (HB == 2 ? (c & 1) * HALO : 0);
+    const uint16_t* hbn = hbase + (HB == 2 ? ((c + 1) & 1) * HALO : 0);
+    const bool next_h = c + 1 < nchunks;
+    const uint16_t* wnext = wsrc + (size_t)(c * 9 + WR - 1) * WSL;
+    auto step = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int sc = t % WR;  // ring slot of slice s = 9c + t
+      // WR = 9: the next chunk's halo goes out first at t = 0, ahead of slice
+      // 9c+8, so the step-7 wait (which retires slice 9c+8) retires it too,
+      // before step 8 reads it
+      if (WR == 9 && HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
+      // slice s+2 (past the end: a dummy re-read of slice 0 into a dead slot)
+      // issue order: slice s+2, then (t = 0) the next chunk's halo into the
+      // other halo buffer (on the last chunk a dummy re-read of this chunk);
+      // glds are LDS writes, so the compiler keeps them in program order
+      // (WR = 9: slice s+8 into the slot of slice s-1, read in step s-1, or
+      // with PB in step s-2)
+      if constexpr (WR == 9)
+        issue_w((t + 8) % 9, (c * 9 + t + 8 < nsteps) ? wnext + t * WSL : wsrc);
+      else if constexpr (PB)
+        issue_w(t % 3, (c * 9 + t + 3 < nsteps) ? wnext + (t + 1) * WSL : wsrc);
+      else
+        issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
+      if (WR == 3 && HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
+      u16x8 bfr[CTW], bnx[CTW];
+      if constexpr (PB) {
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) bfr[ct] = bcur[ct];
+      } else {
+        const uint16_t* wb = wring + sc * WSL;
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
+      }
+      constexpr int kyn = t < 8 ? (t + 1) / 3 : 0, kxn = t < 8 ? (t + 1) % 3 : 0;
+      constexpr int ntoff = PM ? (kyn * RPX + kxn) * 32 : (kyn * HALO_RP + kxn) * 8;
+      const uint16_t* hnx = t < 8 ? hb : hbn;
+      const uint16_t* wbn = wring + ((t + 1) % WR) * WSL;
+#pragma unroll
+      for (int rt = 0; rt < RTW; ++rt) {
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
+        // (HB = 1: the next chunk's tap-0 fragments are read once its halo is in)
+        if (HB == 2 || t < 8) fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
+        if (PB && rt == 0) {
+#pragma unroll
+          for (int ct = 0; ct < CTW; ++ct) bnx[ct] = *(const u16x8*)(wbn + bbase[ct]);
         }
       }
-      const uint16_t* hb = hbase + (HB == 2 ? (c & 1) * HALO : 0);
-      const uint16_t* hbn = hbase + (HB == 2 ? ((c + 1) & 1) * HALO : 0);
-      const bool next_h = c + 1 < nchunks;
-      const uint16_t* wnext = wsrc + (size_t)(c * 9 + WR - 1) * WSL;
-      auto step = [&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        constexpr int sc = t % WR;  // ring slot of slice s = 9c + t
-        // WR = 9: the next chunk's halo goes out first at t = 0, ahead of slice
-        // 9c+8, so the step-7 wait (which retires slice 9c+8) retires it too,
-        // before step 8 reads it
-        if (WR == 9 && HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
-        // slice s+2 (past the end: a dummy re-read of slice 0 into a dead slot)
-        // issue order: slice s+2, then (t = 0) the next chunk's halo into the
-        // other halo buffer (on the last chunk a dummy re-read of this chunk);
-        // glds are LDS writes, so the compiler keeps them in program order
-        // (WR = 9: slice s+8 into the slot of slice s-1, read in step s-1, or
-        // with PB in step s-2)
-        if constexpr (WR == 9)
-          issue_w((t + 8) % 9, (c * 9 + t + 8 < nsteps) ? wnext + t * WSL : wsrc);
-        else if constexpr (PB)
-          issue_w(t % 3, (c * 9 + t + 3 < nsteps) ? wnext + (t + 1) * WSL : wsrc);
-        else
-          issue_w((t + 2) % 3, (c * 9 + t + 2 < nsteps) ? wnext + t * WSL : wsrc);
-        if (WR == 3 && HB == 2 && t == 0) issue_halo(hbase + ((c + 1) & 1) * HALO, next_h ? c + 1 : c);
-        u16x8 bfr[CTW], bnx[CTW];
-        if constexpr (PB) {
+      if constexpr (PB) {
 #pragma unroll
-          for (int ct = 0; ct < CTW; ++ct) bfr[ct] = bcur[ct];
-        } else {
-          const uint16_t* wb = wring + sc * WSL;
+        for (int ct = 0; ct < CTW; ++ct) bcur[ct] = bnx[ct];
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x100, CTW, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, PB ? 1 + CTW : 1, 0);
 #pragma unroll
-          for (int ct = 0; ct < CTW; ++ct) bfr[ct] = *(const u16x8*)(wb + bbase[ct]);
-        }
-        constexpr int kyn = t < 8 ? (t + 1) / 3 : 0, kxn = t < 8 ? (t + 1) % 3 : 0;
-        constexpr int ntoff = PM ? (kyn * RPX + kxn) * 32 : (kyn * HALO_RP + kxn) * 8;
-        const uint16_t* hnx = t < 8 ? hb : hbn;
-        const uint16_t* wbn = wring + ((t + 1) % WR) * WSL;
-#pragma unroll
-        for (int rt = 0; rt < NRT; ++rt) {
-#pragma unroll
-          for (int ct = 0; ct < CTW; ++ct) acc[rt][ct] = T::mfma(fa[rt], bfr[ct], acc[rt][ct]);
-          // (HB = 1: the next chunk's tap-0 fragments are read once its halo is in)
-          if (HB == 2 || t < 8) fa[rt] = *(const u16x8*)(hnx + abase[rt] + ntoff);
-          if (PB && rt == 0) {
-#pragma unroll
-            for (int ct = 0; ct < CTW; ++ct) bnx[ct] = *(const u16x8*)(wbn + bbase[ct]);
-          }
-        }
-        if constexpr (PB) {
-#pragma unroll
-          for (int ct = 0; ct < CTW; ++ct) bcur[ct] = bnx[ct];
-        } else {
-          __builtin_amdgcn_sched_group_barrier(0x100, CTW, 0);
-        }
+      for (int rt = 1; rt < RTW; ++rt) {
         __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, PB ? 1 + CTW : 1, 0);
-#pragma unroll
-        for (int rt = 1; rt < NRT; ++rt) {
-          __builtin_amdgcn_sched_group_barrier(0x008, CTW, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        // Retire slice s+1 (and at t = 1 the next halo), leaving younger glds in
-        // flight; wait + barrier in ONE asm statement, so no LDS access can be
-        // scheduled between this wave's wait and the workgroup barrier.  The LDS
-        // wait retires this step's weight-fragment reads (the ring slot the next
-        // step refills) and leaves the youngest ones, the A-fragment prefetches
-        // for the next tap (halo buffers, not rewritten here), in flight: L of
-        // them (with PB, A(0) sits in one group with the bnx reads).
-        // (WR = 9: slices s+2 .. s+8 and the next halo while t <= 6; with PB,
-        // whose next step reads slice s+2, slices s+3 .. s+8 and the halo
-        // while t <= 5)
-        constexpr int N = WR == 3 ? WPW + (HB == 2 && t <= 1 ? HPW : 0)
-                                  : (PB ? 6 * WPW + (HB == 2 && t <= 5 ? HPW : 0) : 7 * WPW + (HB == 2 && t <= 6 ? HPW : 0));
-        // The relaxed wait relies on the issue order; fac_fake_amd/isa_check.py
-        // verifies it on the built code object (each of the L youngest LDS ops
-        // before every such barrier is a ds_read_b128 whose registers next feed
-        // an MFMA's A operand, no scalar-memory op in the step) and rebuilds
-        // this file with FAC_CONV_STRICT_LGKM (L = 0) if any wait fails.
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      // Retire slice s+1 (and at t = 1 the next halo), leaving younger glds in
+      // flight; wait + barrier in ONE asm statement, so no LDS access can be
+      // scheduled between this wave's wait and the workgroup barrier.  The LDS
+      // wait retires this step's weight-fragment reads (the ring slot the next
+      // step refills) and leaves the youngest ones, the A-fragment prefetches
+      // for the next tap (halo buffers, not rewritten here), in flight: L of
+      // them (with PB, A(0) sits in one group with the bnx reads).
+      // (WR = 9: slices s+2 .. s+8 and the next halo while t <= 6; with PB,
+      // whose next step reads slice s+2, slices s+3 .. s+8 and the halo
+      // while t <= 5)
+      constexpr int N = WR == 3 ? WPW + (HB == 2 && t <= 1 ? HPW : 0)
+                                : (PB ? 6 * WPW + (HB == 2 && t <= 5 ? HPW : 0) : 7 * WPW + (HB == 2 && t <= 6 ? HPW : 0));
+      // The relaxed wait relies on the issue order; fac_fake_amd/isa_check.py
+      // verifies it on the built code object (each of the L youngest LDS ops
+      // before every such barrier is a ds_read_b128 whose registers next feed
+      // an MFMA's A operand, no scalar-memory op in the step) and rebuilds
+      // this file with FAC_CONV_STRICT_LGKM (L = 0) if any wait fails.
 #ifdef FAC_CONV_STRICT_LGKM
-        constexpr int L = 0;
+      constexpr int L = 0;
 #else
-        constexpr int L = (HB == 2 || t < 8) ? (PB ? NRT - 1 : NRT) : 0;
+      constexpr int L = (HB == 2 || t < 8) ? (PB ? RTW - 1 : RTW) : 0;
 #endif
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(%1)\n\ts_barrier" ::"n"(N), "n"(L) : "memory");
-        __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(%1)\n\ts_barrier" ::"n"(N), "n"(L) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #ifdef CONV_STAMPS
-        if (c == 0) CONV_STAMP(2 + t);
+      if (c == 0) CONV_STAMP(2 + t);
 #endif
-      };
-      step(std::integral_constant<int, 0>{});
-      step(std::integral_constant<int, 1>{});
-      step(std::integral_constant<int, 2>{});
-      step(std::integral_constant<int, 3>{});
-      step(std::integral_constant<int, 4>{});
-      step(std::integral_constant<int, 5>{});
-      step(std::integral_constant<int, 6>{});
-      step(std::integral_constant<int, 7>{});
-      step(std::integral_constant<int, 8>{});
-    }
-  };
-  if constexpr (SKIP) {
-    if (__builtin_amdgcn_readfirstlane(wm) == WM - 1)
-      mainloop(std::integral_constant<int, RTW - 1>{});
-    else
-      mainloop(std::integral_constant<int, RTW>{});
-  } else {
-    mainloop(std::integral_constant<int, RTW>{});
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{});
+    step(std::integral_constant<int, 7>{});
+    step(std::integral_constant<int, 8>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // dummy slices land before LDS is reused / the wave ends
   CONV_STAMP(11);
@@ -837,20 +817,20 @@ int conv_block_n(int H, int cout) {
 // POOLED = false: no fused-pool instantiation (the 14x14 / BN 192 tile would
 // spill with it; no model pools after such a layer).
 template <class T, int TH, int TW, int BN, int WM, int WN, int HB = 2, int OCC = 2, bool PB = true, bool POOLED = true,
-          int WR = 3, bool SKIP = false, int RES = 0>
+          int WR = 3>
 static hipError_t launch_box(const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out, int B, int H,
                              int Cin, int Cout, bool pool, const uint16_t* zero16, hipStream_t st, int relu) {
   dim3 grid(B * (H / TH) * (H / TW), Cout / BN);
   if constexpr (POOLED) {
     if (pool) {
-      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, WR, SKIP, RES>
+      conv3x3_bn_relu<T, TH, TW, BN, WM, WN, true, HB, OCC, PB, WR>
           <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
       return hipSuccess;
     }
   } else if (pool) {
     return hipErrorInvalidValue;
   }
-  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, WR, SKIP, RES>
+  conv3x3_bn_relu<T, TH, TW, BN, WM, WN, false, HB, OCC, PB, WR>
       <<<grid, 256, 0, st>>>(in, wpk, bias, out, H, H, Cin, Cout, zero16, relu);
   return hipSuccess;
 }
@@ -890,22 +870,6 @@ static int g_ring9 = 6;
 // CU: conv15-17 0.186 -> 0.196-0.201 ms.  At two workgroups per CU the slice
 // wait is covered; only the one-per-CU grids gain from depth.)
 void set_conv_ring9(int v) { g_ring9 = v; }
-// Wave grid of the 14x14 / BN 128 tile (option "conv14_grid", process-wide,
-// A/B): 0 = 1 x 4 (each wave 13 row tiles x 32 channels), 1 = 2 x 2 (7 row
-// tiles x 64 channels, 14 tiles), 2 = 2 x 2 with the padding tile skipped,
-// 3 = 2 with the B-fragment prefetch (PB), 4 = 1 with PB
-static int g_conv14_grid = 0;
-void set_conv14_grid(int v) { g_conv14_grid = v; }
-// The 28x28 layers with 128-channel blocks (option "conv28_grid", process-wide,
-// A/B; weights packed for BN 128): 0 = conv3x3_db's 4x28 box (1 x 4 waves,
-// B fragments from L2 per wave: 146 B of L2 reads per MFMA, at the CU's L2
-// fetch rate), 1 = four 14x14 boxes per image on the 2 x 2 LDS-ring tile
-// with the padding tile skipped (the slice is shared by two wave rows and
-// 196 pixels: ~100 B per MFMA), 2 = that tile without the skip, 3 = with
-// the B-fragment prefetch
-static int g_conv28_grid = 0;
-void set_conv28_grid(int v) { g_conv28_grid = v; }
-int conv28_grid() { return g_conv28_grid; }
 static int cu_count() {
   static int cached[64] = {0};
   int dev = 0;
@@ -943,35 +907,14 @@ static hipError_t launch_conv_t(const uint16_t* in, const uint16_t* wpk, const f
     case 28256: launch_db<T, 4, 28, 256, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28192: launch_db<T, 4, 28, 192, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
     case 28128:
-      if (g_conv28_grid && !few) {
-        switch (g_conv28_grid) {
-          case 2:
-            launch_box<T, 14, 14, 128, 2, 2, 2, 2, false, true, 3, false, 28>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-            break;
-          case 3:
-            launch_box<T, 14, 14, 128, 2, 2, 2, 2, true, true, 3, false, 28>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-            break;
-          default:
-            launch_box<T, 14, 14, 128, 2, 2, 2, 2, false, true, 3, true, 28>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-        }
-      } else if (ring9 & 4)
+      if (ring9 & 4)
         launch_db<T, 4, 28, 128, 1, 4, 2, 9>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       else
         launch_db<T, 4, 28, 128, 1, 4>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       break;
     // (a two-box 14x14 workgroup needs 256+ VGPRs and spills: not built)
     case 14128:
-      switch (g_conv14_grid) {
-        case 1: launch_box<T, 14, 14, 128, 2, 2, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-        case 2:
-          launch_box<T, 14, 14, 128, 2, 2, 2, 2, false, true, 3, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-          break;
-        case 3:
-          launch_box<T, 14, 14, 128, 2, 2, 2, 2, true, true, 3, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-          break;
-        case 4: launch_box<T, 14, 14, 128, 2, 2, 2, 2, true>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu); break;
-        default: launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
-      }
+      launch_box<T, 14, 14, 128, 1, 4, 2, 2, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu);
       break;
     case 14192:
       if (launch_box<T, 14, 14, 192, 1, 4, 2, 2, false, false>(in, wpk, bias, out, B, H, Cin, Cout, pool, z, st, relu) != hipSuccess)

@@ -23,9 +23,6 @@
 
 namespace fac {
 void set_conv_ring9(int v);
-void set_conv14_grid(int v);
-void set_conv28_grid(int v);
-int conv28_grid();
 int conv_block_n(int H, int cout);
 void set_nd_pt_wide(int v);
 void set_gemm_small(int max_m, int variant);
@@ -273,11 +270,6 @@ hipError_t run_conv(const fac_ctx* c, const ConvLayer& L, const uint16_t* in, ui
   if (L.w_small32 && c->conv_small && c->small14 && (long long)B * (L.Cout / 32) <= c->num_cu)
     return launch_conv3x3(c->dtype, in, L.w_small32, L.b, out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st, true,
                           32);
-  // option conv28_grid: the 28^2 layers on 128-channel blocks for every B
-  // (launch_conv_t picks the 14x14-box tile, or conv3x3_db for few crops)
-  if (L.H == 28 && L.w_small && L.bn_small == 128 && conv28_grid())
-    return launch_conv3x3(c->dtype, in, L.w_small, L.b, out, B, L.H, L.H, L.Cin, L.Cout, L.pool, c->zero16, st, true,
-                          128);
   if (L.w_small && c->conv_small) {
     const int bn = conv_block_n(L.H, L.Cout), boxes = L.H == 14 ? 1 : (L.H / 4) * (L.H / 28);
     if ((long long)B * boxes * (L.Cout / bn) < c->num_cu)
@@ -998,16 +990,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "conv_ring9") {  // process-wide A/B: 9-slice weight ring (bit 0: the 14x14 / BN 64 tile)
     if (value < 0 || value > 7) return set_err(c, FAC_ERR_ARG, "conv_ring9 must be 0..7");
     fac::set_conv_ring9(value);
-    return FAC_OK;
-  }
-  if (k == "conv28_grid") {  // process-wide A/B: the 28x28 layers' 128-channel tile (conv.hip)
-    if (value < 0 || value > 3) return set_err(c, FAC_ERR_ARG, "conv28_grid must be 0..3");
-    fac::set_conv28_grid(value);
-    return FAC_OK;
-  }
-  if (k == "conv14_grid") {  // process-wide A/B: wave grid of the 14x14 / BN 128 conv tile (conv.hip)
-    if (value < 0 || value > 4) return set_err(c, FAC_ERR_ARG, "conv14_grid must be 0..4");
-    fac::set_conv14_grid(value);
     return FAC_OK;
   }
   if (k == "conv_small14") {

@@ -209,14 +209,7 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * crops; the default; 0 = the 64-channel blocks only; bit-identical).
  * Process-wide knobs of the fac_ops.h layer kernels (A/B measurements; any
  * context sets them; every fac_set_option call makes every context recapture
- * its small-batch graphs before their next replay): "conv14_grid" (wave grid
- * of the 14x14 / BN-128 conv tile: 0 = 1 x 4, 1 = 2 x 2, 2 = 2 x 2 with the
- * padding row tile skipped, 3 = 2 with the B-fragment prefetch, 4 = 1 with
- * it; bit-identical outputs), "conv28_grid" (the 28x28 layers on 128-channel
- * blocks: 0 = conv3x3_db's 4x28 box, the default; 1 = four 14x14 boxes per
- * image on the 2 x 2 LDS-ring tile, padding tile skipped; 2 = without the
- * skip; 3 = with the B-fragment prefetch; few-crop grids keep conv3x3_db;
- * bit-identical outputs), "conv_ring9" (0..7, bit mask of
+ * its small-batch graphs before their next replay): "conv_ring9" (0..7, bit mask of
  * the conv kernels that take a 9-slice weight ring when the grid is at most 2
  * workgroups per CU, i.e. few crops: bits 0 and 1 the two 9-slice variants
  * of the 14x14 BN-64 tile (bit 1 wins), bit 2 the 28x28 conv3x3_db register

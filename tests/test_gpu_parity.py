@@ -816,77 +816,6 @@ def test_few_crop_forward_equals_full_batch(models, dt):
     assert np.array_equal(off, small)
 
 
-@pytest.mark.parametrize("B", [64, 70])
-def test_conv14_grid_is_bit_identical(models, B):
-    """Option conv14_grid (the wave grid of the 14x14 / BN-128 conv tile: 1 x 4,
-    2 x 2, 2 x 2 skipping the padding row tile, with / without the B-fragment
-    prefetch) only changes which wave computes which (pixel, channel) tiles;
-    each output keeps its k order, so conv14-17's outputs and the logits are
-    bit-identical in both dtypes (B >= 64: the BN-128 grid, not the few-crop
-    blocks; 70: a ragged last XCD range)."""
-    from fac_fake_amd import _lib
-    lib = _lib.load()
-    x = torch.from_numpy(make_crops(B, seed=91)).to(DEV)
-    pidx = (torch.arange(B) % 32).to(torch.int32)
-    for dt in ("fp16", "bf16"):
-        m = models[dt]
-        tdt = torch.float16 if dt == "fp16" else torch.bfloat16
-        outs = {}
-        try:
-            for v in (0, 1, 2, 3, 4):
-                m.set_option("conv14_grid", v)
-                feats = []
-                for layer, shape in ((13, (B, 14, 14, 512)), (14, (B, 14, 14, 512)), (16, (B, 7, 7, 512))):
-                    f = torch.empty(*shape, dtype=tdt, device=DEV)
-                    _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), B, layer, f.data_ptr(), None), m._ctx,
-                               "dbg")
-                    feats.append(f.view(torch.int16).cpu())
-                lg = m.forward_u8(x, pos_index=pidx)
-                torch.cuda.synchronize()
-                outs[v] = (feats, lg.cpu())
-        finally:
-            m.set_option("conv14_grid", 0)
-        for v in (1, 2, 3, 4):
-            for a, b in zip(outs[0][0], outs[v][0]):
-                assert torch.equal(a, b), (dt, v)
-            assert torch.equal(outs[0][1], outs[v][1]), (dt, v)
-
-
-@pytest.mark.parametrize("B", [9, 64, 70])
-def test_conv28_grid_is_bit_identical(models, B):
-    """Option conv28_grid (the 28^2 layers on 128-channel blocks: conv3x3_db's
-    4x28 box, or four 14x14 boxes per image on the 2 x 2 LDS-ring tile, with
-    or without the padding-tile skip / the B-fragment prefetch) keeps every
-    output's k order: conv10-13's outputs and the logits are bit-identical in
-    both dtypes (B = 9: the few-crop rule keeps conv3x3_db)."""
-    from fac_fake_amd import _lib
-    lib = _lib.load()
-    x = torch.from_numpy(make_crops(B, seed=97)).to(DEV)
-    pidx = (torch.arange(B) % 32).to(torch.int32)
-    for dt in ("fp16", "bf16"):
-        m = models[dt]
-        tdt = torch.float16 if dt == "fp16" else torch.bfloat16
-        outs = {}
-        try:
-            for v in (0, 1, 2, 3):
-                m.set_option("conv28_grid", v)
-                feats = []
-                for layer, shape in ((9, (B, 28, 28, 256)), (10, (B, 28, 28, 256)), (12, (B, 14, 14, 256))):
-                    f = torch.empty(*shape, dtype=tdt, device=DEV)
-                    _lib.check(lib.fac_debug_features_u8(m._ctx, x.data_ptr(), B, layer, f.data_ptr(), None), m._ctx,
-                               "dbg")
-                    feats.append(f.view(torch.int16).cpu())
-                lg = m.forward_u8(x, pos_index=pidx)
-                torch.cuda.synchronize()
-                outs[v] = (feats, lg.cpu())
-        finally:
-            m.set_option("conv28_grid", 0)
-        for v in (1, 2, 3):
-            for a, b in zip(outs[0][0], outs[v][0]):
-                assert torch.equal(a, b), (dt, v)
-            assert torch.equal(outs[0][1], outs[v][1]), (dt, v)
-
-
 @pytest.mark.parametrize("B", [3, 29])
 def test_ring9_conv_is_bit_identical(models, B):
     """Option conv_ring9 (the few-crop 14^2 / 28^2 convs with 9-slice weight
