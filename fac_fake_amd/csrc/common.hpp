@@ -42,6 +42,10 @@ struct BF16 {
     const bf16x2 hi = __builtin_convertvector((f32x2){v[2], v[3]}, bf16x2);
     return __builtin_bit_cast(u16x4, __builtin_shufflevector(lo, hi, 0, 1, 2, 3));
   }
+  // 2 floats -> two 16-bit values in one dword (low = a), one v_cvt_pk_bf16_f32
+  __device__ __forceinline__ static uint32_t pack2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+  }
   __device__ __forceinline__ static f32x4 mfma(u16x8 a, u16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
@@ -62,6 +66,9 @@ struct F16 {
     const f16x2 lo = __builtin_convertvector((f32x2){v[0], v[1]}, f16x2);
     const f16x2 hi = __builtin_convertvector((f32x2){v[2], v[3]}, f16x2);
     return __builtin_bit_cast(u16x4, __builtin_shufflevector(lo, hi, 0, 1, 2, 3));
+  }
+  __device__ __forceinline__ static uint32_t pack2(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, f16x2));
   }
   __device__ __forceinline__ static f32x4 mfma(u16x8 a, u16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),

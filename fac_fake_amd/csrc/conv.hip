@@ -111,10 +111,15 @@ __device__ __forceinline__ void stage_tile(const f32x4 (&acc)[RTW][CTW], uint16_
         f32x4 y;
 #pragma unroll
         for (int j = 0; j < 4; ++j) y[j] = RELU ? relu(v[j] + bv) : v[j] + bv;
-        const u16x4 p = T::pack4(y);
+        // rows (0,1) and (2,3) as two packed dwords: one conversion per pair,
+        // the high halves stored by ds_write_b16_d16_hi (as a u16x4 the
+        // compiler converted every value on its own, one cvt each)
+        const uint32_t p01 = T::pack2(y[0], y[1]), p23 = T::pack2(y[2], y[3]);
         const int m0 = (wm * RTW + rt) * 16 + (lane >> 4) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ostg[(m0 + j) * OPS + nl] = p[j];
+        ostg[(m0 + 0) * OPS + nl] = (uint16_t)p01;
+        ostg[(m0 + 1) * OPS + nl] = (uint16_t)(p01 >> 16);
+        ostg[(m0 + 2) * OPS + nl] = (uint16_t)p23;
+        ostg[(m0 + 3) * OPS + nl] = (uint16_t)(p23 >> 16);
       }
     }
   }

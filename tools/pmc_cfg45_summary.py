@@ -37,6 +37,7 @@ def summarise(src: Path, model: str, forwards: int) -> dict:
     kernels = sorted(set().union(*[set(p) for p in passes]))
     res = {"by_kernel": {}, "forward": {}}
     tot = defaultdict(float)
+    setup = defaultdict(float)  # non-fac dispatches (one-time workspace memset, input copies): kept out of the totals
     for k in kernels:
         vals = {}
         n = 0
@@ -45,6 +46,8 @@ def summarise(src: Path, model: str, forwards: int) -> dict:
                 vals[c] = sum(v) / len(v)
                 if k.startswith("fac::"):  # runtime copies / torch fills: one-time setup, not the forward
                     tot[c] += sum(v)
+                else:
+                    setup[c] += sum(v)
                 n = max(n, len(v))
         m = {"dispatches": n, **{c: round(v, 1) for c, v in vals.items()}, **derive(vals)}
         if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
@@ -57,6 +60,10 @@ def summarise(src: Path, model: str, forwards: int) -> dict:
         res["forward"]["kernel_cycles_per_forward"] = round(tot["GRBM_GUI_ACTIVE"] / 8 / forwards)
     if tot.get("FETCH_SIZE"):
         res["forward"]["hbm_bytes_per_forward"] = round((2 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0 / forwards)
+        res["forward"]["hbm_bytes_per_forward_counts"] = "fac:: kernels only"
+        res["forward"]["excluded_setup_hbm_bytes_total"] = round((2 * setup.get("FETCH_SIZE", 0.0) +
+                                                                  setup.get("WRITE_SIZE", 0.0)) * 1024.0)
+        res["forward"]["excluded_setup_kernels"] = sorted(k for k in kernels if not k.startswith("fac::"))
     res["forwards_profiled"] = forwards
     res["method"] = ("rocprofv3 --pmc, one run per pass (tools/pmc_cfg45.sh) over the eager forwards of "
                      "tools/rvk_layers.py; mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8)")
