@@ -553,7 +553,7 @@ struct Prof {
 };
 
 int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, float* logits, float* probs,
-              hipStream_t st, Prof* prof, float* hidden_out = nullptr);
+              hipStream_t st, Prof* prof, float* hidden_out = nullptr, bool beside_stack = false);
 
 // The synchronous forward on `stream`: conv stack -> stem_dst (default the
 // context's stem buffer 0), then (unless conv_only) the encoder and head.
@@ -703,9 +703,13 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
 // Patch embedding, the 6 encoder layers and the head on `st`, from the conv
 // stack's output `stem` [B,7,7,512] (cvit.py:171-179).
 int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, float* logits, float* probs,
-              hipStream_t st, Prof* prof, float* hidden_out) {
+              hipStream_t st, Prof* prof, float* hidden_out, bool beside_stack) {
   using namespace fac;
   const int dt = c->dtype;
+  // beside_stack: this encoder co-runs with the next batch's conv stack (the
+  // pipelined forward): the default tile rule for that case (launch_gemm, -2)
+  int gv[6];
+  for (int i = 0; i < 6; ++i) gv[i] = (beside_stack && c->gemm_var[i] == -1) ? -2 : c->gemm_var[i];
 #define MARK(sid)                                  \
   do {                                             \
     if (prof) {                                    \
@@ -718,7 +722,7 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
   } while (0)
   const int S = patch_splits(B);
   HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, stem, kPatchDim, c->pe_w, kPatchDim, nullptr, c->slab, kDim, B, kDim,
-                         kPatchDim, S, st, c->gemm_var[0]));
+                         kPatchDim, S, st, gv[0]));
   // residual stream rows + layer 0's PreNorm LayerNorm in one pass
   HIP_TRY(c, launch_embed_finalize_ln(dt, c->slab, S, B, c->pe_b, c->cls, c->pos, pidx, c->x, c->tl[0].ln1_g,
                                       c->tl[0].ln1_b, c->xn, c->errflag, ++c->fwd_seq, st));
@@ -735,21 +739,21 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
       HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, c->tl[l - 1].b2, T.ln1_g, T.ln1_b, c->xn, R, st));
     }
     HIP_TRY(c, launch_gemm(dt, EPI_F32, c->xn, kDim, T.wqkv, kDim, nullptr, c->qkv, 3 * kDim, R, 3 * kDim, kDim, 1, st,
-                           c->gemm_var[1]));
+                           gv[1]));
     HIP_TRY(c, launch_attention2(dt, c->qkv, c->o, B, scale, st));
     HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->o, kDim, T.wo, kDim, nullptr, c->slab, kDim, R, kDim, kDim, SK, st,
-                           c->gemm_var[2]));
+                           gv[2]));
     HIP_TRY(c, launch_resid_layernorm(dt, c->x, c->slab, SK, T.bo, T.ln2_g, T.ln2_b, c->xn, R, st, c->ffn_ln_eps));
     HIP_TRY(c, launch_gemm(dt, EPI_T_GELU, c->xn, kDim, T.w1, kDim, T.b1, c->hbuf, kMlp, R, kMlp, kDim, 1, st,
-                           c->gemm_var[3]));
-    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->hbuf, kMlp, T.w2, kMlp, nullptr, c->slab, kDim, R, kDim, kMlp, SK, st, c->gemm_var[4]));
+                           gv[3]));
+    HIP_TRY(c, launch_gemm(dt, EPI_PARTIAL, c->hbuf, kMlp, T.w2, kMlp, nullptr, c->slab, kDim, R, kDim, kMlp, SK, st, gv[4]));
   }
   MARK(18);
   HIP_TRY(c, launch_resid_cls(dt, c->x, c->slab, SK, c->tl[kDepth - 1].b2, c->cbuf, B, st));
   // hidden_out: the ReLU'd first head layer is the result (ResVitKan's KAN head follows)
   float* hh = hidden_out ? hidden_out : c->hh;
   HIP_TRY(c, launch_gemm(dt, EPI_F32_RELU, c->cbuf, kDim, c->h1_w, kDim, c->h1_b, hh, kMlp, B, kMlp, kDim, 1, st,
-                         c->gemm_var[5]));
+                         gv[5]));
   if (logits) HIP_TRY(c, launch_head_out(hh, c->h2_w, c->h2_b, logits, probs, B, st));
   MARK(19);
 #undef MARK
@@ -1148,7 +1152,7 @@ int fac_forward_nhwc_u8_pipelined(fac_ctx* c, const uint8_t* d_in, int B, const 
   if (rc) return rc;
   HIP_TRY(c, hipEventRecord(c->ev_conv[k], st));
   HIP_TRY(c, hipStreamWaitEvent(c->tail_st, c->ev_conv[k], 0));
-  rc = tail_impl(c, stem, B, d_pos, d_logits, d_probs, c->tail_st, nullptr);
+  rc = tail_impl(c, stem, B, d_pos, d_logits, d_probs, c->tail_st, nullptr, nullptr, true);
   if (rc) return rc;
   if (d_score) HIP_TRY(c, fac::launch_video_score(d_logits, B, d_score, c->tail_st));
   HIP_TRY(c, hipEventRecord(c->ev_tail[k], c->tail_st));

@@ -509,16 +509,23 @@ void set_gemm_small(int max_m, int variant) {
   kSmallVariant = variant;
 }
 
-// variant < 0: pick by shape.  Measured on MI355X (tools/gemm_sweep.py, bf16,
-// B = 256): the 32x128 / ring-3 tile (2 WG/CU) wins every encoder GEMM
-// (M = 512, K = 1024..2048: QKV 11.1 us, FF1 11.5, FF2/4 7.1, head 8.7 vs
-// 13-18 us for 64x128); deeper rings at 1 WG/CU lose.  The long-K patch
-// GEMM (K = 25088, split 14) prefers 64x128 / ring 3 (28.5 us).
+// variant < 0: pick by shape.  Alone (tools/gemm_sweep.py, bf16, B = 256) the
+// 32x128 / ring-3 tile (2 WG/CU) wins the encoder GEMMs at M = 512 rows
+// (K = 1024..2048: QKV 11.1 us, FF1 11.5, FF2/4 7.1, head 8.7 vs 13-18 us for
+// 64x128); the long-K patch GEMM (K = 25088, split 14) and every GEMM with
+// more than 1024 rows take 64x128 / ring 3 (ResVitKan's 3072-crop encoder,
+// M = 6144: +1.2 %, profiles/r06_tail_gemm_ab.txt).  variant -2: the encoder
+// that runs beside the next batch's conv stack (the software pipeline,
+// fac_forward_nhwc_u8_pipelined), where what counts is the CU time its
+// workgroups take from the convs: the 64x128 tile at every M > kSmallM (half
+// the workgroups, each A row read once per 128 columns instead of per 32
+// rows x 128; headline +0.2 to +1.7 %, same-box alternations, same file).
 hipError_t launch_gemm(int dtype, int epi, const uint16_t* A, int lda, const uint16_t* W, int ldw, const float* bias,
                        void* out, int ldo, int M, int N, int K, int splits, hipStream_t st, int variant) {
   if (N % 128 != 0 || splits < 1 || K % (64 * splits) != 0 || M <= 0 || epi < 0 || epi > EPI_T)
     return hipErrorInvalidValue;
-  if (variant < 0) variant = M <= kSmallM ? kSmallVariant : (K / splits >= 1024 && K >= 8192 ? 0 : 2);
+  if (variant < 0)
+    variant = M <= kSmallM ? kSmallVariant : ((variant == -2 || M > 1024 || (K / splits >= 1024 && K >= 8192)) ? 0 : 2);
   if (variant >= kGemmVariants) return hipErrorInvalidValue;
   if (dtype == 0) return launch_gemm_t<BF16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, variant, st);
   return launch_gemm_t<F16>(epi, A, lda, W, ldw, bias, out, ldo, M, N, K, splits, variant, st);

@@ -193,7 +193,9 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
 /* Named knobs: "stem_chunk" (as above), "fuse_stem224" (1 = conv1..conv3 +
  * pool as one fused kernel, the default; 0 = one kernel per conv),
  * "gemm_patch" / "gemm_qkv" / "gemm_out" / "gemm_ff1" / "gemm_ff2" /
- * "gemm_head" (GEMM tile variant -1..6 per call site), "proj_splits" (split-K
+ * "gemm_head" (GEMM tile variant 0..6 per call site; -1, the default, picks
+ * by shape: 64x32 at <= 64 rows, 64x128 above 1024 rows, in the pipelined
+ * forward's encoder and for the patch GEMM, else 32x128), "proj_splits" (split-K
  * of to_out and FF2: 1, 2 or 4), "tail_only" (before fac_load_weights: no
  * conv stem, fac_forward_features only), "tail_priority", "stem_events" (1 =
  * time every fused-stem launch, fac_stem_event_ms), "stem_nwg" (persistent
