@@ -137,24 +137,6 @@ struct fac_ctx {
   // head run on tail_st, ordered by ev_conv[k&1] / ev_tail[k&1]
   hipStream_t tail_st = nullptr;
   hipEvent_t ev_conv[2] = {nullptr, nullptr}, ev_tail[2] = {nullptr, nullptr};
-  // The pipelined forward defers batch k's encoder until batch k+1's fused
-  // stem has finished (ev_stem_done, recorded by forward_impl when
-  // rec_stem_done is set): enqueued right behind conv17, the high-priority
-  // encoder kept a CU busy somewhere at every moment and the stem -- one
-  // whole-CU workgroup per CU -- could not start until the encoder paused,
-  // ~0.25 ms of the conv stream idle per 3 ms step (r05 kernel trace,
-  // DESIGN.md §5).  ptail: the batch whose encoder is not enqueued yet; every
-  // other entry point enqueues it first (flush_tail), so its results are
-  // complete after fac_pipeline_join as before.
-  struct PendingTail {
-    bool valid = false;
-    int k = 0, B = 0;
-    uint16_t* stem = nullptr;
-    const int32_t* pos = nullptr;
-    float *logits = nullptr, *probs = nullptr, *score = nullptr;
-  } ptail;
-  hipEvent_t ev_stem_done = nullptr;
-  bool rec_stem_done = false;
   bool tail_pending[2] = {false, false};
   int pipe_k = 0;
   int tail_priority = 1;  // option "tail_priority": 1 = high-priority tail stream
@@ -334,8 +316,6 @@ WsLayout layout(int B, int chunk) {
   return L;
 }
 
-int flush_tail(fac_ctx* c, bool after_stem = false);
-
 // Drop the captured small-batch graphs (they hold the workspace and weight
 // pointers and the kernel choices of the options they were captured with):
 // on a workspace reallocation, a weight load, an option change or destroy.
@@ -349,7 +329,6 @@ void drop_graphs(fac_ctx* c) {
 
 int ensure_ws(fac_ctx* c, int B) {
   if (B <= c->cap_B && c->ws) return FAC_OK;
-  if (int e = flush_tail(c)) return e;  // it reads a stem buffer of the workspace about to be freed
   drop_graphs(c);
   const WsLayout L = layout(B, c->stem_chunk);
   if (c->ws) {
@@ -576,23 +555,6 @@ struct Prof {
 int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, float* logits, float* probs,
               hipStream_t st, Prof* prof, float* hidden_out = nullptr, bool beside_stack = false);
 
-// Enqueue the deferred encoder of the pipelined forward (fac_ctx::ptail) on
-// the tail stream: after its own conv stack (ev_conv) and, if after_stem,
-// after the next batch's stem (ev_stem_done).
-int flush_tail(fac_ctx* c, bool after_stem) {
-  if (!c->ptail.valid) return FAC_OK;
-  const fac_ctx::PendingTail p = c->ptail;
-  c->ptail.valid = false;
-  HIP_TRY(c, hipStreamWaitEvent(c->tail_st, c->ev_conv[p.k], 0));
-  if (after_stem) HIP_TRY(c, hipStreamWaitEvent(c->tail_st, c->ev_stem_done, 0));
-  const int rc = tail_impl(c, p.stem, p.B, p.pos, p.logits, p.probs, c->tail_st, nullptr, nullptr, true);
-  if (rc) return rc;
-  if (p.score) HIP_TRY(c, fac::launch_video_score(p.logits, p.B, p.score, c->tail_st));
-  HIP_TRY(c, hipEventRecord(c->ev_tail[p.k], c->tail_st));
-  c->tail_pending[p.k] = true;
-  return FAC_OK;
-}
-
 // The synchronous forward on `stream`: conv stack -> stem_dst (default the
 // context's stem buffer 0), then (unless conv_only) the encoder and head.
 int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx, float* logits, float* probs,
@@ -634,7 +596,6 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
   if (!stem_dst) {
     // a synchronous forward shares the encoder workspace with pipelined
     // tails still in flight: order it after them
-    if (int e = flush_tail(c)) return e;
     stem_dst = c->stem_out;
     for (int i = 0; i < 2; ++i)
       if (c->tail_pending[i]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[i], 0));
@@ -684,7 +645,6 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
       HIP_TRY(c, launch_stem224(dt, u8, src, c->conv1_wp, c->conv1_b, c->conv[0].w, c->conv[0].b, c->conv[1].w,
                                 c->conv[1].b, cur, nb, c->stem_nwg > 0 ? c->stem_nwg : c->num_cu, st));
       if (sev1) HIP_TRY(c, hipEventRecord(sev1, st));
-      if (c->rec_stem_done && b0 == 0) HIP_TRY(c, hipEventRecord(c->ev_stem_done, st));
       MARK(0);
       l0 = 2;
       if (stop_after == 2) {
@@ -705,7 +665,6 @@ int forward_impl(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pidx
       const ConvLayer& L = c->conv[l];
       uint16_t* dst = (l == kLastChunked) ? c->deep0 + (size_t)b0 * conv_out_elems(L) : nxt;
       HIP_TRY(c, run_conv(c, L, cur, dst, nb, st));
-      if (c->rec_stem_done && b0 == 0 && l == 1) HIP_TRY(c, hipEventRecord(c->ev_stem_done, st));
       MARK(l + 1);
       if (stop_after == l + 1 && l != kLastChunked) {
         HIP_TRY(c, hipMemcpyAsync(feat_out + (size_t)b0 * conv_out_elems(L), dst, (size_t)nb * conv_out_elems(L) * 2,
@@ -804,7 +763,6 @@ int tail_impl(fac_ctx* c, const uint16_t* stem, int B, const int32_t* pidx, floa
 // Order work enqueued on `st` after the context's previous forward on another
 // stream and after any pipelined tail still in flight (fac_ctx::ev_stack).
 int order_on(fac_ctx* c, hipStream_t st) {
-  if (int e = flush_tail(c)) return e;
   if (!c->ev_stack) HIP_TRY(c, hipEventCreateWithFlags(&c->ev_stack, hipEventDisableTiming));
   if (c->stack_rec && c->stack_st != st) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_stack, 0));
   for (int i = 0; i < 2; ++i)
@@ -857,7 +815,6 @@ int forward_graph(fac_ctx* c, const void* in, bool u8, int B, const int32_t* pid
                   hipStream_t st) {
   if (int e = take_device_error(c)) return e;
   DevGuard g(c->device);
-  if (int e = flush_tail(c)) return e;  // before any capture: the deferred encoder is not captured
   int rc = ensure_ws(c, B);
   if (rc) return rc;
   if (const unsigned gen = g_knob_gen.load(); gen != c->knob_gen) {
@@ -989,7 +946,6 @@ int fac_create(int device, int dtype, fac_ctx** out) {
 int fac_load_weights(fac_ctx* c, const fac_tensor_desc* descs, int n) {
   if (!c || !descs || n <= 0) return set_err(c, FAC_ERR_ARG, "bad load arguments");
   DevGuard g(c->device);
-  if (int e = flush_tail(c)) return e;  // the deferred encoder runs on the weights it was submitted with
   drop_graphs(c);
   for (void* p : c->weights) (void)hipFree(p);
   c->weights.clear();
@@ -1031,7 +987,6 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   {  // every knob can change what a captured forward would launch -- in this
      // context, and for the process-wide ones in every other (g_knob_gen)
     DevGuard g(c->device);
-    if (int e = flush_tail(c)) return e;  // with the kernels of the options it was submitted under
     drop_graphs(c);
     c->knob_gen = ++g_knob_gen;
   }
@@ -1140,7 +1095,6 @@ int fac_forward_features(fac_ctx* c, const void* d_feat, int B, const int32_t* d
   if (B > 32 * 1024) return set_err(c, FAC_ERR_SHAPE, "batch too large");
   if (int e = take_device_error(c)) return e;
   DevGuard g(c->device);
-  if (int e = flush_tail(c)) return e;
   int rc = ensure_ws(c, B);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
@@ -1184,38 +1138,25 @@ int fac_forward_nhwc_u8_pipelined(fac_ctx* c, const uint8_t* d_in, int B, const 
       HIP_TRY(c, hipEventCreateWithFlags(&c->ev_conv[i], hipEventDisableTiming));
       HIP_TRY(c, hipEventCreateWithFlags(&c->ev_tail[i], hipEventDisableTiming));
     }
-    HIP_TRY(c, hipEventCreateWithFlags(&c->ev_stem_done, hipEventDisableTiming));
   }
-  if (B > c->cap_B && (c->ptail.valid || c->tail_pending[0] || c->tail_pending[1])) {
-    if (int e = flush_tail(c)) return e;
+  if (B > c->cap_B && (c->tail_pending[0] || c->tail_pending[1]))
     HIP_TRY(c, hipStreamSynchronize(c->tail_st));  // the workspace is about to be reallocated
-  }
   int rc = ensure_ws(c, B);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   const int k = c->pipe_k & 1;
   uint16_t* stem = k ? c->stem_out2 : c->stem_out;
-  // stem buffer k was last read by the encoder of batch k-2 (enqueued by the
-  // previous call, behind this buffer's previous stem)
+  // stem buffer k was last read by the tail of batch k-2
   if (c->tail_pending[k]) HIP_TRY(c, hipStreamWaitEvent(st, c->ev_tail[k], 0));
-  // this batch's conv stack; the previous batch's encoder then starts once
-  // this stack's fused stem is done (ev_stem_done), so it co-runs with conv4
-  // .. conv17 instead of holding the stem off the CUs
-  const bool defer = c->ptail.valid;
-  c->rec_stem_done = defer;
   rc = forward_impl(c, d_in, true, B, nullptr, nullptr, nullptr, stream, nullptr, -1, nullptr, nullptr, stem, true);
-  c->rec_stem_done = false;
   if (rc) return rc;
   HIP_TRY(c, hipEventRecord(c->ev_conv[k], st));
-  if (defer && (rc = flush_tail(c, true))) return rc;
-  c->ptail.valid = true;
-  c->ptail.k = k;
-  c->ptail.B = B;
-  c->ptail.stem = stem;
-  c->ptail.pos = d_pos;
-  c->ptail.logits = d_logits;
-  c->ptail.probs = d_probs;
-  c->ptail.score = d_score;
+  HIP_TRY(c, hipStreamWaitEvent(c->tail_st, c->ev_conv[k], 0));
+  rc = tail_impl(c, stem, B, d_pos, d_logits, d_probs, c->tail_st, nullptr, nullptr, true);
+  if (rc) return rc;
+  if (d_score) HIP_TRY(c, fac::launch_video_score(d_logits, B, d_score, c->tail_st));
+  HIP_TRY(c, hipEventRecord(c->ev_tail[k], c->tail_st));
+  c->tail_pending[k] = true;
   c->pipe_k++;
   return FAC_OK;
 }
@@ -1224,10 +1165,6 @@ int fac_pipeline_join(fac_ctx* c, int keep, void* stream) {
   if (!c || keep < 0) return FAC_ERR_ARG;
   if (!c->tail_st) return FAC_OK;
   DevGuard g(c->device);
-  // the most recent batch's encoder is the deferred one (fac_ctx::ptail):
-  // enqueue it now unless it is among the `keep` not waited for
-  if (keep == 0)
-    if (int e = flush_tail(c)) return e;
   // the batches enqueued, oldest first: pipe_k-2, pipe_k-1 (slots (pipe_k-2)&1, (pipe_k-1)&1)
   for (int age = 2; age > keep; --age) {
     const int k = (c->pipe_k - age) & 1;
@@ -1340,7 +1277,6 @@ void fac_destroy(fac_ctx* c) {
         (void)hipEventDestroy(c->ev_conv[i]);
         (void)hipEventDestroy(c->ev_tail[i]);
       }
-      (void)hipEventDestroy(c->ev_stem_done);
     }
     for (hipEvent_t e : c->stem_evs) (void)hipEventDestroy(e);
     if (c->ev_stack) (void)hipEventDestroy(c->ev_stack);
