@@ -799,6 +799,204 @@ __global__ __launch_bounds__(256) void maxpool3_lds14(fac_pool_desc p) {
   }
 }
 
+// ---- maxpool3_pw (round 6): S3D's Inception branch3 -- MaxPool3d(3, 1, 1)
+// then BasicConv3d(cin, cout, 1) + BN + ReLU (model.py:84-342, e.g.
+// :100-103) -- as one launch, so the pooled map (as large as the block
+// input) is never written to HBM and read back.  A unit is (clip, G
+// consecutive frames) of an S x S map; per 64-channel chunk of the input:
+//  1. every (position, 16-byte piece) of the unit takes the max over its
+//     frames z-1..z+1 (three global loads, clamped to the clip: a max over a
+//     repeat) into an LDS image (double-buffered, one barrier per chunk);
+//  2. each wave then forms its MFMA B fragments directly: a 16-lane row of
+//     a fragment holds whole image rows (16 / S of them, lane = x), so the
+//     max over y-1..y+1 is three LDS reads and the max over x-1..x+1 two DPP
+//     row shifts (neighbours outside the row: the lane itself);
+//  3. the fragments feed the 1x1 conv's MFMAs straight from registers
+//     (weights [n][k] read as A fragments from global / L1, transposed as in
+//     conv_pw: each lane ends with 8 consecutive channels of one position).
+// Maxima are exact (a max selects one of its inputs), taken on the 16-bit
+// patterns: fp16 with v_pk_max_f16, bf16 as int16 keys (x ^ 0x7fff for
+// negative x, monotonic in the float order) with v_pk_max_i16.  Outputs are
+// what fac_pool_nd then the 1x1 conv produce, up to fp32 summation order and
+// the sign of a zero.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <class T>
+__device__ __forceinline__ uint32_t mp_key(uint32_t v) {  // an involution
+  if constexpr (T::id == 0) {
+    const s16x2 s = __builtin_bit_cast(s16x2, v);
+    return __builtin_bit_cast(uint32_t, s ^ ((s >> (s16x2)15) & (s16x2)0x7fff));
+  } else {
+    return v;
+  }
+}
+template <class T>
+__device__ __forceinline__ uint32_t mp_max(uint32_t a, uint32_t b) {
+  if constexpr (T::id == 0)
+    return __builtin_bit_cast(uint32_t,
+                              __builtin_elementwise_max(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b)));
+  else
+    return __builtin_bit_cast(uint32_t,
+                              __builtin_elementwise_max(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b)));
+}
+template <class T>
+__device__ __forceinline__ u32x4 mp_max4(u32x4 a, u32x4 b) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = mp_max<T>(a[i], b[i]);
+  return r;
+}
+
+// S: map side; G: frames per unit (divides the clip's frames); NCT: output
+// channels per workgroup / 32 (blockIdx.y walks the column blocks)
+template <class T, int S, int G, int NCT>
+__global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                      const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                      int nunits, int D, int C, int kp, int ldo, int c_off,
+                                                      int relu_on) {
+  constexpr int P = G * S * S;              // positions per unit
+  constexpr int RPT = 16 / S;               // image rows per 16-lane fragment row
+  constexpr int NR = G * S;                 // image rows per unit
+  constexpr int NT = (NR + RPT - 1) / RPT;  // MFMA position tiles per unit
+  constexpr int RTW = (NT + 3) / 4;         // per wave
+  constexpr int NIT = (P * 8 + 255) / 256;  // phase-1 items per thread
+  constexpr int TMS = P * 64;               // elements per LDS image
+  constexpr int CT = 2 * NCT;               // 16-channel MFMA tiles
+  __shared__ __attribute__((aligned(16))) uint16_t tm[2 * TMS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  // units dealt to XCDs in contiguous ranges (block b runs on XCD b % 8), so
+  // the frames a unit shares with its neighbours are re-read from one L2
+  const int per = (int)(gridDim.x >> 3);
+  const int u = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (u >= nunits) return;
+  const int n0 = blockIdx.y * 32 * NCT;
+  const int ngr = D / G, clip = u / ngr, z0 = (u - clip * ngr) * G;
+  const int fs = S * S * C;
+  const uint16_t* xb = in + (size_t)clip * D * fs;
+
+  // phase 1 geometry: item q = (position p, piece c8): the element offset of
+  // its centre frame, and packed: LDS slot | c8 << 16 (8: no item) | frame
+  // z-1 in the clip << 20 | frame z+1 in the clip << 21
+  int qoff[NIT], qinf[NIT];
+#pragma unroll
+  for (int j = 0; j < NIT; ++j) {
+    const int q = tid + 256 * j, p = q >> 3, c8 = q & 7;
+    const int zz = p / (S * S), pos = p - zz * S * S, z = z0 + zz;
+    qoff[j] = z * fs + pos * C + c8 * 8;
+    qinf[j] = (p * 8 + (c8 ^ ((p >> 1) & 7))) * 8 | (q < P * 8 ? c8 : 8) << 16 | (z > 0) << 20 | (z + 1 < D) << 21;
+  }
+  // phase 2 geometry: this lane's image row within a fragment row and column
+  const int lr = r16 < RPT * S ? r16 / S : RPT - 1, x = r16 < RPT * S ? r16 - lr * S : S - 1;
+  const bool xl = x == 0, xr = x == S - 1;
+  // weight rows: fragment row r16 of channel tile ct = channel
+  // 32 (ct >> 1) + 8 (r16 >> 2) + 4 (ct & 1) + (r16 & 3) (conv_pw's order)
+  const uint16_t* wrow[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+    wrow[ct] = w + (size_t)(n0 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3)) * kp + g * 8;
+
+  f32x4 acc[RTW][CT];
+#pragma unroll
+  for (int i = 0; i < RTW; ++i)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[i][ct] = (f32x4)0.f;
+
+  const int nch = kp / 64;
+  for (int kc = 0; kc < nch; ++kc) {
+    uint16_t* const img = tm + (kc & 1) * TMS;
+    const int kb = kc * 64, nval = min(8, (C - kb) >> 3);  // valid pieces of this chunk
+    // 1. frame maxima into the image (pieces past C: zero, which the zero
+    // weight rows of k_pad multiply)
+    u32x4 v[NIT][3];
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+      if (((qinf[j] >> 16) & 15) < nval) {
+        const uint16_t* c = xb + qoff[j] + kb;
+        v[j][0] = *(const u32x4*)(c - ((qinf[j] >> 20) & 1) * fs);
+        v[j][1] = *(const u32x4*)c;
+        v[j][2] = *(const u32x4*)(c + ((qinf[j] >> 21) & 1) * fs);
+      } else {
+        v[j][0] = v[j][1] = v[j][2] = (u32x4)0u;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) {
+      if (((qinf[j] >> 16) & 15) >= 8) continue;
+      u32x4 m;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        m[i] = mp_max<T>(mp_max<T>(mp_key<T>(v[j][0][i]), mp_key<T>(v[j][1][i])), mp_key<T>(v[j][2][i]));
+      *(u32x4*)(img + (qinf[j] & 0xffff)) = m;
+    }
+    // this chunk's weight fragments, in flight across the barrier
+    u16x8 wf[2][CT];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) wf[s][ct] = *(const u16x8*)(wrow[ct] + kb + s * 32);
+    __syncthreads();
+    // 2 + 3. row and column maxima into B fragments, MFMAs
+#pragma unroll
+    for (int i = 0; i < RTW; ++i) {
+      const int t = wave + 4 * i;
+      if (t >= NT) break;
+      const int rho = min(t * RPT + lr, NR - 1), y = rho % S, p = rho * S + x;
+      const int pu = y > 0 ? p - S : p, pd = y + 1 < S ? p + S : p;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int c8 = s * 4 + g;
+        const u32x4 a = *(const u32x4*)(img + (pu * 8 + (c8 ^ ((pu >> 1) & 7))) * 8);
+        const u32x4 b = *(const u32x4*)(img + (p * 8 + (c8 ^ ((p >> 1) & 7))) * 8);
+        const u32x4 c = *(const u32x4*)(img + (pd * 8 + (c8 ^ ((pd >> 1) & 7))) * 8);
+        const u32x4 vm = mp_max4<T>(mp_max4<T>(a, b), c);
+        u32x4 f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t ve = vm[e];
+          uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp((int)ve, (int)ve, 0x111, 0xf, 0xf, false);  // row_shr:1
+          uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp((int)ve, (int)ve, 0x101, 0xf, 0xf, false);  // row_shl:1
+          l = xl ? ve : l;
+          r = xr ? ve : r;
+          f[e] = mp_key<T>(mp_max<T>(mp_max<T>(l, ve), r));
+        }
+        const u16x8 pf = __builtin_bit_cast(u16x8, f);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) acc[i][ct] = T::mfma(wf[s][ct], pf, acc[i][ct]);
+      }
+    }
+  }
+  // epilogue: bias + ReLU, 16-byte stores of channels n0 + 32 h + 8 g .. + 7
+  float bv[CT][4];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[n0 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
+  if (r16 >= RPT * S) return;
+#pragma unroll
+  for (int i = 0; i < RTW; ++i) {
+    const int t = wave + 4 * i, rho = t * RPT + lr;
+    if (t >= NT || rho >= NR) break;
+    uint16_t* o = out + (size_t)(u * P + rho * S + x) * ldo + c_off + n0 + 8 * g;
+#pragma unroll
+    for (int h = 0; h < NCT; ++h) {
+      u16x4 q[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        f32x4 vv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float z = acc[i][2 * h + e][j] + bv[2 * h + e][j];
+          vv[j] = relu_on ? relu(z) : z;
+        }
+        q[e] = T::pack4(vv);
+      }
+      *(u16x8*)(o + 32 * h) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+}
+
 // ---- input staging
 template <class T, bool U8>
 __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
@@ -3069,6 +3267,46 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     else
       conv_s2d4_mp<F16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
                                               (uint16_t*)d->out, nstrip, d->h, d->w, hp, wp, k_pad);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  // MaxPool3d(3, 1, 1) over the input, then this 1x1x1 conv (S3D's
+  // Inception branch3): maxpool3_pw
+  if (d->flags & FAC_CONV_MAXPOOL3S1) {
+    const int S = d->h;
+    if (split || (d->flags & ~(FAC_CONV_RELU | FAC_CONV_MAXPOOL3S1)) || d->kd != 1 || d->kh != 1 || d->kw != 1 ||
+        d->sd != 1 || d->sh != 1 || d->sw != 1 || d->pd || d->ph || d->pw || d->w != S ||
+        !(S == 14 || S == 7 || S == 3) || d->cout % 32 || d->ldo % 8 || d->c_off % 8)
+      return FAC_ERR_ARG;
+    // frames per unit: 196 positions at 7 x 7 when the clip allows, 18 at 3 x 3
+    const int G = S == 14 ? 1 : (S == 7 ? (d->d % 4 == 0 ? 4 : (d->d % 2 == 0 ? 2 : 1)) : (d->d % 2 == 0 ? 2 : 1));
+    const int nunits = d->n * (d->d / G);
+    const int nct = d->cout % 64 == 0 ? 2 : 1;
+    const dim3 grid((nunits + 7) / 8 * 8, d->cout / (32 * nct));
+    const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
+    const uint16_t* in = (const uint16_t*)d->in;
+    const uint16_t* wt = (const uint16_t*)d->weight;
+    uint16_t* o = (uint16_t*)d->out;
+#define FAC_MPW(TT, SS, GG, NN)                                                                                     \
+  maxpool3_pw<TT, SS, GG, NN><<<grid, 256, 0, st>>>(in, wt, d->bias, o, nunits, d->d, d->cin, k_pad, d->ldo, d->c_off, \
+                                                     relu_on)
+#define FAC_MPW_S(TT, NN)                      \
+  do {                                         \
+    if (S == 14) FAC_MPW(TT, 14, 1, NN);       \
+    else if (S == 7 && G == 4) FAC_MPW(TT, 7, 4, NN); \
+    else if (S == 7 && G == 2) FAC_MPW(TT, 7, 2, NN); \
+    else if (S == 7) FAC_MPW(TT, 7, 1, NN);    \
+    else if (G == 2) FAC_MPW(TT, 3, 2, NN);    \
+    else FAC_MPW(TT, 3, 1, NN);                \
+  } while (0)
+    if (d->dtype == FAC_DTYPE_BF16) {
+      if (nct == 2) FAC_MPW_S(BF16, 2);
+      else FAC_MPW_S(BF16, 1);
+    } else {
+      if (nct == 2) FAC_MPW_S(F16, 2);
+      else FAC_MPW_S(F16, 1);
+    }
+#undef FAC_MPW_S
+#undef FAC_MPW
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   // the space-to-depth first conv (4x4/1 over 16-channel cells, cout 64, no

@@ -197,6 +197,9 @@ class S3D(nn.Module):
     # multiple of 64 (padt), so their (3,1,1) halves take the uniform-tap gather
     pad64_level = 1
     padt = True
+    # branch3's MaxPool3d(3, 1, 1) fused into its 1x1x1 conv (FAC_CONV_MAXPOOL3S1)
+    # on the 14 / 7 / 3 maps; False: fac_pool_nd then the conv (A/B)
+    fuse_pool3 = True
 
     def _pad64(self, c: int, level: int) -> int:
         if self.pad64_level < level or c % 64 == 0 or (level == 1 and c < 64):
@@ -209,7 +212,8 @@ class S3D(nn.Module):
         three 1x1x1 heads (branch0.0, branch1.0, branch2.0) as one
         column-split launch (ops.conv_split: branch0 straight into its slot),
         then branch1's and branch2's SepConvs, then branch3's MaxPool3d(3,1,1)
-        + 1x1x1.  (The branches on concurrent side streams measured faster or
+        + 1x1x1 (one launch where maxpool3_pw covers the map: the pooled map
+        never goes through memory).  (The branches on concurrent side streams measured faster or
         slower depending on which hardware queues torch's pool streams land on
         -- 27.0k vs 20.5k clips/s for the same graph -- so the serial order is
         the dependable one.)"""
@@ -232,7 +236,11 @@ class S3D(nn.Module):
         conv_split(blk["heads" + sfx], x, blk["head_splits" + sfx], out, 0, h1, h2)
         t1(s1(h1), out=out, c_off=o1)
         t2(s2(h2), out=out, c_off=o2)
-        blk["b3"](max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
+        b3 = blk["b3"]
+        if self.fuse_pool3 and b3.maxpool3s1_ok(x, out, o3):
+            b3(x, out=out, c_off=o3, maxpool3s1=True)       # pool + 1x1x1 in one launch (ops.hip maxpool3_pw)
+        else:
+            b3(max_pool_sep(x, 3, 1, 1), out=out, c_off=o3)
         return out
 
     def features16(self, x16: torch.Tensor, taps: list | None = None) -> torch.Tensor:

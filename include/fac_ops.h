@@ -34,6 +34,15 @@ extern "C" {
                                 first conv below (ResNet-50's conv1 + bn1 +
                                 relu + maxpool, ResVitKan.py:187/205);
                                 FAC_ERR_ARG otherwise */
+#define FAC_CONV_MAXPOOL3S1 32 /* MaxPool3d(3, 1, 1) over the INPUT first
+                                (-inf padding), then the conv: a 1x1x1 conv
+                                (stride 1, no padding) over an S x S map,
+                                S in {14, 7, 3}, cout % 32 == 0, ldo and
+                                c_off % 8 == 0, flags FAC_CONV_RELU at most
+                                besides this one; FAC_ERR_ARG otherwise.
+                                S3D's Inception branch3 (MaxPool3d +
+                                BasicConv3d(cin, cout, 1), model.py:84-342)
+                                without the pooled map in memory */
 
 /* One N-d convolution (Conv2d / Conv3d, any kernel, stride, zero padding,
  * dilation 1, groups 1) with folded BatchNorm, as an implicit GEMM on MFMA:

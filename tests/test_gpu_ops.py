@@ -425,6 +425,49 @@ def test_max_pool_3x3x3_s1_lds14(dt, d, c):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("n,d,h,cin,cout,c_off", [
+    (2, 8, 14, 192, 32, 8),      # Mixed_3b branch3 at 112^2 clips (one 32-channel block)
+    (3, 8, 14, 256, 64, 0),      # Mixed_3c
+    (3, 5, 14, 64, 64, 16),      # 4b at the harness's 20 x 224^2 clips: 5 frames
+    (3, 4, 7, 480, 64, 16),      # 4b at 112^2: K chunks of 64 with a half-empty last one, 4 frames per unit
+    (2, 4, 7, 528, 128, 0),      # 4f: two column blocks, a quarter-full last chunk
+    (2, 2, 7, 512, 64, 8),       # two frames per unit
+    (2, 5, 7, 64, 96, 0),        # one frame per unit, three 32-channel blocks
+    (3, 2, 3, 832, 128, 0),      # 5b / 5c at 112^2: 3 x 3 maps
+    (2, 3, 3, 64, 32, 8),
+])
+def test_conv_maxpool3s1_fused(n, d, h, cin, cout, c_off, dt):
+    """FAC_CONV_MAXPOOL3S1 (ops.hip maxpool3_pw): S3D's Inception branch3,
+    MaxPool3d(3, 1, 1) then a 1x1x1 conv + bias + ReLU in one launch, into a
+    channel slot of a wider tensor.  Against PyTorch fp32 of the same 16-bit
+    operands (the pool is exact in 16 bits) within one 16-bit ulp, against
+    fac_pool_nd + the conv's own kernel within one ulp, and the neighbouring
+    channels untouched.  Inputs of both signs (the bf16 max runs on int16
+    keys), units that do not fill the last XCD range."""
+    from fac_fake_amd.ops import ConvLayer, max_pool_sep
+    g = torch.Generator().manual_seed(31 + d + h + cin + cout)
+    x = torch.randn(n, cin, d, h, h, generator=g).to(T16[dt]).float()
+    wt = torch.randn(cout, cin, 1, 1, 1, generator=g) / np.sqrt(cin)
+    b = torch.randn(cout, generator=g) * 0.1
+    layer = ConvLayer(wt, b, 1, 0, dtype=dt, device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    assert layer.maxpool3s1_ok(xg)
+    big = torch.zeros(n, d, h, h, cout + 24, dtype=T16[dt], device=DEV)
+    layer(xg, relu=True, out=big, c_off=c_off, maxpool3s1=True)
+    unf = layer(max_pool_sep(xg, 3, 1, 1), relu=True)
+    torch.cuda.synchronize()
+    pooled = F.max_pool3d(x, 3, 1, 1)
+    ref = F.relu(F.conv3d(pooled, wt.to(T16[dt]).float(), b)).permute(0, 2, 3, 4, 1).to(T16[dt])
+    bc = big.cpu()
+    got = bc[..., c_off:c_off + cout]
+    u = _ulps(got, ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05, float(u.max())
+    assert _ulps(got, unf.cpu(), dt).max() <= 1.0
+    assert bc[..., :c_off].abs().max() == 0 if c_off else True
+    assert bc[..., c_off + cout:].abs().max() == 0
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("h,w,pb,pa", [(30, 26, 2, 1), (224, 224, 2, 1), (18, 16, 0, 0)])
 def test_pack_input_s2d_u8_cells(h, w, pb, pa, dt):
     """fac_pack_input_s2d on uint8 NHWC images (ResNet-50's conv1 input,

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--u8", action="store_true", help="uint8 clips (decoded frames: base.0 as one launch)")
     ap.add_argument("--no-fuse", action="store_true", help="with --u8: base.0 as two launches")
+    ap.add_argument("--no-pool3", action="store_true", help="branch3's MaxPool3d(3,1,1) as its own launch")
     ap.add_argument("--opt", action="append", default=[], help="process-wide fac_set_option knob, name=value")
     a = ap.parse_args()
     if a.opt:
@@ -42,6 +43,7 @@ def main():
     if a.u8:
         clips = clips.to(torch.uint8)
     m.fuse_base0 = not a.no_fuse
+    m.fuse_pool3 = not a.no_pool3
     for _ in range(a.reps):
         m(clips)
         torch.cuda.synchronize()
