@@ -864,6 +864,7 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
   constexpr int TMS = P * 64;               // elements per LDS image
   constexpr int CT = 2 * NCT;               // 16-channel MFMA tiles
   __shared__ __attribute__((aligned(16))) uint16_t tm[2 * TMS];
+  __shared__ __attribute__((aligned(16))) uint16_t wl[2][2 * CT * 512];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   // units dealt to XCDs in contiguous ranges (block b runs on XCD b % 8), so
@@ -890,12 +891,20 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
   // phase 2 geometry: this lane's image row within a fragment row and column
   const int lr = r16 < RPT * S ? r16 / S : RPT - 1, x = r16 < RPT * S ? r16 - lr * S : S - 1;
   const bool xl = x == 0, xr = x == S - 1;
-  // weight rows: fragment row r16 of channel tile ct = channel
-  // 32 (ct >> 1) + 8 (r16 >> 2) + 4 (ct & 1) + (r16 & 3) (conv_pw's order)
-  const uint16_t* wrow[CT];
+  // weight fragments: row r16 of channel tile ct = channel
+  // 32 (ct >> 1) + 8 (r16 >> 2) + 4 (ct & 1) + (r16 & 3) (conv_pw's order);
+  // a chunk's 2 x CT fragments (k-step s, tile ct) are copied to LDS by
+  // global_load_lds, fragment f = s * CT + ct by wave f % 4, each a 1 KB
+  // lane-ordered image [g][r16][8] (one conflict-free ds_read_b128 per use),
+  // double-buffered: issued with the chunk's pixel loads, so a chunk costs
+  // one memory round trip and no VGPRs hold weights across it
+  constexpr int WFW = (2 * CT + 3) / 4;  // fragments per wave per chunk
+  const uint16_t* wsrc[WFW];
 #pragma unroll
-  for (int ct = 0; ct < CT; ++ct)
-    wrow[ct] = w + (size_t)(n0 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3)) * kp + g * 8;
+  for (int i = 0; i < WFW; ++i) {
+    const int f = wave + 4 * i, ct = f % CT, s = f / CT;
+    wsrc[i] = w + (size_t)(n0 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3)) * kp + s * 32 + g * 8;
+  }
 
   f32x4 acc[RTW][CT];
 #pragma unroll
@@ -907,6 +916,10 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
   for (int kc = 0; kc < nch; ++kc) {
     uint16_t* const img = tm + (kc & 1) * TMS;
     const int kb = kc * 64, nval = min(8, (C - kb) >> 3);  // valid pieces of this chunk
+    uint16_t* const wimg = wl[kc & 1];
+#pragma unroll
+    for (int i = 0; i < WFW; ++i)
+      if (wave + 4 * i < 2 * CT) glds16(wsrc[i] + kb, wimg + (wave + 4 * i) * 512);
     // 1. frame maxima into the image (pieces past C: zero, which the zero
     // weight rows of k_pad multiply)
     u32x4 v[NIT][3];
@@ -930,13 +943,7 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
         m[i] = mp_max<T>(mp_max<T>(mp_key<T>(v[j][0][i]), mp_key<T>(v[j][1][i])), mp_key<T>(v[j][2][i]));
       *(u32x4*)(img + (qinf[j] & 0xffff)) = m;
     }
-    // this chunk's weight fragments, in flight across the barrier
-    u16x8 wf[2][CT];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) wf[s][ct] = *(const u16x8*)(wrow[ct] + kb + s * 32);
-    __syncthreads();
+    __syncthreads();  // (its vmcnt(0) also lands the weight fragments)
     // 2 + 3. row and column maxima into B fragments, MFMAs
 #pragma unroll
     for (int i = 0; i < RTW; ++i) {
@@ -963,7 +970,8 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
         }
         const u16x8 pf = __builtin_bit_cast(u16x8, f);
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) acc[i][ct] = T::mfma(wf[s][ct], pf, acc[i][ct]);
+        for (int ct = 0; ct < CT; ++ct)
+          acc[i][ct] = T::mfma(*(const u16x8*)(wimg + (s * CT + ct) * 512 + lane * 8), pf, acc[i][ct]);
       }
     }
   }

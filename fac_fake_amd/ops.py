@@ -171,13 +171,18 @@ class ConvLayer:
             self._pk33[h] = pk
         return self._pk33[h]
 
+    # maps the S3D drop-in fuses branch3's pool on: the kernel also takes 3 x 3,
+    # where the chain of 13 dependent 64-channel chunks per unit measured
+    # slower than the pool + conv launches (94 vs ~59 us at 1536 clips)
+    MAXPOOL3S1_MAPS = (14, 7)
+
     def maxpool3s1_ok(self, x: torch.Tensor, out: torch.Tensor | None = None, c_off: int = 0) -> bool:
         """Whether fac_conv_nd takes FAC_CONV_MAXPOOL3S1 for this layer on x
         (ops.hip maxpool3_pw)."""
         g = self.g
         _, _, h, w, _ = x.shape
         return ((g.kd, g.kh, g.kw, g.sd, g.sh, g.sw, g.pd, g.ph, g.pw) == (1, 1, 1, 1, 1, 1, 0, 0, 0)
-                and h == w and h in (14, 7, 3) and self.cout % 32 == 0 and c_off % 8 == 0
+                and h == w and h in self.MAXPOOL3S1_MAPS and self.cout % 32 == 0 and c_off % 8 == 0
                 and (out is None or out.shape[4] % 8 == 0) and _lib.exports("fac_conv_nd"))
 
     def out_dims(self, d, h, w):

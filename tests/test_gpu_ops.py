@@ -450,6 +450,7 @@ def test_conv_maxpool3s1_fused(n, d, h, cin, cout, c_off, dt):
     wt = torch.randn(cout, cin, 1, 1, 1, generator=g) / np.sqrt(cin)
     b = torch.randn(cout, generator=g) * 0.1
     layer = ConvLayer(wt, b, 1, 0, dtype=dt, device=DEV)
+    layer.MAXPOOL3S1_MAPS = (14, 7, 3)   # the ABI's maps (the S3D drop-in fuses 14 and 7)
     xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
     assert layer.maxpool3s1_ok(xg)
     big = torch.zeros(n, d, h, h, cout + 24, dtype=T16[dt], device=DEV)
