@@ -2417,6 +2417,155 @@ __global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ i
   }
 }
 
+// ---- pw_res (round 6): ResNet-50's bottleneck conv3 with its identity --
+// relu(relu(conv1x1(x) + b3) + x_in) (ResVitKan.py:146-152, torchvision's
+// Bottleneck) -- for layer2's 128 -> 512 and layer3's 256 -> 1024.  These
+// move 2.25 KB / 4.5 KB of HBM per position (input row, residual and output
+// rows) for 0.13 / 0.5 MFLOP: HBM-bound, but convnd_pt ran them at 3.9 /
+// 3.4 TB/s against the 5.9 TB/s torch's own add of the same residual and
+// output streams reaches on the same box (tools/res_ceiling.py): its K steps
+// stream 256-wide weight slices through LDS for a 2-4-step K.  Here one
+// 512-thread workgroup per CU keeps its BN x K weight block resident in LDS
+// (64 KB, loaded once) and walks BM-row tiles of one column block; the next
+// tile's input rows AND its BM x BN residual block go global -> LDS
+// (global_load_lds, double-buffered) while this tile computes, so each tile
+// waits only for bytes issued a whole tile earlier.  MFMAs transposed (rows =
+// channels, conv_pw's channel order): a lane ends with 8 consecutive
+// channels of a position, read its residual with one ds_read_b128 and stores
+// 16 bytes.  LDS rows keep 16-byte piece p at p ^ (row & 15) (conflict-free
+// for the fragment and residual reads: 16 rows of one piece column hit 16
+// distinct bank groups).  LDS: weights 64 KB + 2 x input tile + 2 x residual
+// tile = 160 KB for both instances.
+template <class T, int KC, int BN, int BM>
+__global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                 const float* __restrict__ bias, const uint16_t* __restrict__ res,
+                                                 uint16_t* __restrict__ out, int M, int kp, int ldo, int c_off, int ldr,
+                                                 int r_off, int ny, int relu1, int relu2) {
+  constexpr int K = KC * 32, PPR = K / 8, RPR = BN / 8;  // 16-byte pieces per input / residual row
+  constexpr int NW = 8, WN = BN / 64, WM = NW / WN, WPOS = BM / WM, PT = WPOS / 16;
+  constexpr int WEL = BN * K, AEL = BM * K, REL = BM * BN;  // elements
+  constexpr int APL = BM * PPR / 512, RPL = BM * RPR / 512;  // glds pieces per lane per tile
+  constexpr int SL = 2 * PT;                                 // 16-byte stores per lane per tile
+  static_assert(PT >= 1 && WPOS % 16 == 0 && APL * 512 == BM * PPR && RPL * 512 == BM * RPR, "tile shape");
+  static_assert(PPR >= 16 && RPR >= 16, "piece swizzle spans 16 slots");
+  static_assert(2 * (WEL + 2 * AEL + 2 * REL) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * AEL + 2 * REL];
+  uint16_t* const sw = smem;
+  uint16_t* const sa = smem + WEL;
+  uint16_t* const sr = sa + 2 * AEL;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int wn = wave % WN, wm = wave / WN;
+  const int G = gridDim.x;
+  int b = blockIdx.x;
+  if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);  // consecutive b on one XCD: a row tile's column blocks share its L2
+  const int cb = b % ny, rstep = G / ny, n0 = cb * BN;
+  const int nrt = (M + BM - 1) / BM;
+
+  // the column block's weights, fragment (wn', k-step s, channel tile ct) as
+  // a lane-ordered 1 KB image [g][r16][8]: row r16 of tile ct = channel
+  // 32 (ct >> 1) + 8 (r16 >> 2) + 4 (ct & 1) + (r16 & 3) of group wn'
+  for (int f = wave; f < WN * KC * 4; f += NW) {
+    const int ct = f & 3, s = (f >> 2) % KC, wq = f / (4 * KC);
+    const int n = n0 + wq * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
+    *(u16x8*)(sw + f * 512 + lane * 8) = *(const u16x8*)(w + (size_t)n * kp + s * 32 + g * 8);
+  }
+  float bv[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bv[h][j] = bias ? bias[n0 + wn * 64 + 32 * h + 8 * g + j] : 0.f;
+  // glds geometry: wave instruction i fills 64 consecutive 16-byte LDS units
+  // q = (i NW + wave) 64 + lane of a tile image: row q / PR, slot q % PR,
+  // holding the row's piece slot ^ (row & 15)
+  int arow[APL], aoff[APL], rrow[RPL], roff[RPL];
+#pragma unroll
+  for (int i = 0; i < APL; ++i) {
+    const int q = (i * NW + wave) * 64 + lane, r = q / PPR, j = q - r * PPR;
+    arow[i] = r;
+    aoff[i] = (j ^ (r & 15)) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < RPL; ++i) {
+    const int q = (i * NW + wave) * 64 + lane, r = q / RPR, j = q - r * RPR;
+    rrow[i] = r;
+    roff[i] = r_off + n0 + (j ^ (r & 15)) * 8;
+  }
+  // a tile's input rows and residual block into buffer buf.  Rows past M
+  // re-read row M - 1 (their outputs go to the sink) and tiles past the end
+  // re-read tile 0 into a buffer never read: every lane always issues APL +
+  // RPL pieces per tile from valid rows, branch-free, so the vmcnt counts
+  // below hold
+  auto issue = [&](int tile, int buf) {
+    const int m0 = tile < nrt ? tile * BM : 0;
+#pragma unroll
+    for (int i = 0; i < APL; ++i) {
+      const int m = min(m0 + arow[i], M - 1);
+      glds16(in + (size_t)m * K + aoff[i], sa + buf * AEL + (i * NW + wave) * 64 * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int m = min(m0 + rrow[i], M - 1);
+      glds16(res + (size_t)m * ldr + roff[i], sr + buf * REL + (i * NW + wave) * 64 * 8);
+    }
+  };
+  __syncthreads();  // weights in
+  int rt = b / ny;
+  if (rt < nrt) issue(rt, 0);
+  for (int it = 0; rt < nrt; ++it, rt += rstep) {
+    const int buf = it & 1;
+    // this tile's pieces landed; younger: the previous tile's SL stores
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(SL) : "memory");
+    issue(rt + rstep, buf ^ 1);  // its readers (the previous tile) passed the barrier
+    const uint16_t* a = sa + buf * AEL;
+    f32x4 acc[PT][4];
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = (f32x4)0.f;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      u16x8 wf[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) wf[ct] = *(const u16x8*)(sw + ((wn * KC + s) * 4 + ct) * 512 + lane * 8);
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) {
+        const int r = wm * WPOS + pt * 16 + r16;
+        const u16x8 pf = *(const u16x8*)(a + (r * PPR + ((s * 4 + g) ^ (r & 15))) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = T::mfma(wf[ct], pf, acc[pt][ct]);
+      }
+    }
+    // epilogue: v = relu?(acc + b3) + residual, relu?; 16-byte stores of
+    // channels n0 + 64 wn + 32 h + 8 g .. +7
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) {
+      const int r = wm * WPOS + pt * 16 + r16, m = rt * BM + r;
+      uint16_t* o = m < M ? out + (size_t)m * ldo + c_off + n0 + wn * 64 + 8 * g : g_sink + lane * 8;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const u16x8 rv = *(const u16x8*)(sr + buf * REL + (r * RPR + ((wn * 8 + 4 * h + g) ^ (r & 15))) * 8);
+        u16x4 q[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          f32x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float x = acc[pt][2 * h + e][j] + bv[h][4 * e + j];
+            if (relu1) x = relu(x);
+            x += T::to_f32(rv[4 * e + j]);
+            if (relu2) x = relu(x);
+            v[j] = x;
+          }
+          q[e] = T::pack4(v);
+        }
+        *(u16x8*)(m < M ? o + 32 * h : o) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+  }
+}
+
 // ---- conv_tk: S3D's temporal (kd,1,1) convs with 8 output frames (model.py:
 // 63-82, SepConv3d's conv_t + bn_t + relu_t: base.0's (7,1,1)/(2,1,1) and
 // base.3's (3,1,1) at 56^2 / 28^2 positions).  Through the generic implicit
@@ -3105,6 +3254,10 @@ void set_pool3_zg(int v) { g_pool3_zg = v; }
 // process-wide (fac_set_option "pool_lds14"): 1 (default) MaxPool3d(3,1,1) on
 // 14 x 14 maps with 64-multiple channels by maxpool3_lds14, 0 maxpool3_s1
 static int g_pool_lds14 = 1;
+// process-wide (fac_set_option "pw_res"): 1 (default) the K = 128 / 256
+// bottleneck conv3 + identity by pw_res, 0 by convnd_pt (A/B)
+static int g_pw_res = 1;
+void set_pw_res(int v) { g_pw_res = v; }
 void set_pool_lds14(int v) { g_pool_lds14 = v; }
 
 template <class T>
@@ -3329,6 +3482,34 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     else
       conv_s2d4<F16><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,
                                            (uint16_t*)d->out, nbox, d->h, d->w, d->oh, d->ow, k_pad, relu_on);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  // the bottleneck conv3 + identity at K = 128 / 256 (ResNet-50 layer2 /
+  // layer3, relu(relu(conv + b) + residual)): pw_res
+  if (g_pw_res && !split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+      d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->flags & FAC_CONV_RESID) &&
+      !(d->flags & ~(FAC_CONV_RELU | FAC_CONV_RESID | FAC_CONV_RELU2)) && k_pad == d->cin &&
+      ((d->cin == 128 && d->cout % 256 == 0) || (d->cin == 256 && d->cout % 128 == 0)) && d->ldo % 8 == 0 &&
+      d->c_off % 8 == 0 && d->ldr % 8 == 0 && d->r_off % 8 == 0) {
+    const int bn = d->cin == 128 ? 256 : 128, ny = d->cout / bn;
+    const int ncu = cu_count();
+    const int G = std::max(ny, ncu / ny * ny);
+    const int r1 = (d->flags & FAC_CONV_RELU) != 0, r2 = (d->flags & FAC_CONV_RELU2) != 0;
+    const uint16_t* in = (const uint16_t*)d->in;
+    const uint16_t* wt = (const uint16_t*)d->weight;
+    const uint16_t* res = (const uint16_t*)d->residual;
+    uint16_t* o = (uint16_t*)d->out;
+    const int mi = (int)M;
+#define FAC_PWR(TT, KC, BNN) \
+  pw_res<TT, KC, BNN, 64><<<G, 512, 0, st>>>(in, wt, d->bias, res, o, mi, k_pad, d->ldo, d->c_off, d->ldr, d->r_off, ny, r1, r2)
+    if (d->dtype == FAC_DTYPE_BF16) {
+      if (d->cin == 128) FAC_PWR(BF16, 4, 256);
+      else FAC_PWR(BF16, 8, 128);
+    } else {
+      if (d->cin == 128) FAC_PWR(F16, 4, 256);
+      else FAC_PWR(F16, 8, 128);
+    }
+#undef FAC_PWR
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   // stride-1 1x1 convs with K = cin in {64, 128, 256}: conv_pw

@@ -270,6 +270,60 @@ def test_conv_pw_residual_into_slot(cin, cout, dt):
     assert bc[..., :8].abs().max() == 0 and bc[..., 8 + cout:].abs().max() == 0
 
 
+def _set_knob(name: bytes, value: int, dt: str):
+    """A process-wide fac_set_option knob (any context sets it)."""
+    import ctypes
+    from fac_fake_amd import _lib
+    lib = _lib.load()
+    h = ctypes.c_void_p()
+    _lib.check(lib.fac_create(0, _lib.DTYPES[dt], ctypes.byref(h)), None, "fac_create")
+    try:
+        _lib.check(lib.fac_set_option(h, name, value), h, "fac_set_option")
+    finally:
+        lib.fac_destroy(h)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("n,h,w,cin,cout", [
+    (3, 23, 29, 128, 512),     # layer2's conv3 shape class, 2001 positions: a ragged last 64-row tile
+    (2, 14, 14, 256, 1024),    # layer3
+    (1, 37, 41, 256, 256),     # two 128-wide column blocks, ragged
+    (2, 9, 7, 128, 256),       # fewer row tiles than workgroups: most walk nothing
+])
+def test_pw_res_bottleneck_conv3(n, h, w, cin, cout, dt):
+    """pw_res (ResNet's conv3 + bn3 + ReLU + identity + ReLU at K = 128 /
+    256: weights resident in LDS, input rows and residual blocks streamed by
+    global_load_lds) into a channel slot of a wider buffer: against PyTorch
+    fp32 of the same 16-bit operands within one 16-bit ulp, against the
+    convnd_pt route (fac_set_option pw_res = 0) within one ulp, the channels
+    around the slot untouched."""
+    from fac_fake_amd.ops import ConvLayer
+    g = torch.Generator().manual_seed(5 + cin + cout + h)
+    x = torch.randn(n, cin, 1, h, w, generator=g).to(T16[dt]).float()
+    wt = torch.randn(cout, cin, 1, 1, 1, generator=g) / np.sqrt(cin)
+    b = torch.randn(cout, generator=g) * 0.1
+    res = torch.randn(n, 1, h, w, cout, generator=g).to(T16[dt])
+    layer = ConvLayer(wt, b, 1, 0, dtype=dt, device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    outs = {}
+    try:
+        for v in (1, 0):
+            _set_knob(b"pw_res", v, dt)
+            big = torch.full((n, 1, h, w, cout + 16), 3.0, dtype=T16[dt], device=DEV)
+            layer(xg, relu=True, out=big, c_off=8, residual=res.to(DEV), relu2=True)
+            torch.cuda.synchronize()
+            outs[v] = big.cpu()
+    finally:
+        _set_knob(b"pw_res", 1, dt)
+    conv = F.conv3d(x, wt.to(T16[dt]).float(), b).permute(0, 2, 3, 4, 1)
+    ref = F.relu(F.relu(conv) + res.float()).to(T16[dt])
+    bc = outs[1]
+    u = _ulps(bc[..., 8:8 + cout], ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05, float(u.max())
+    assert _ulps(bc, outs[0], dt).max() <= 1.0
+    assert torch.all(bc[..., :8] == 3.0) and torch.all(bc[..., 8 + cout:] == 3.0)
+
+
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", [
     # (n, h, cin3, hx, cin_ds, stride_ds, cout): ResNet-50 bottleneck conv3 + downsample
