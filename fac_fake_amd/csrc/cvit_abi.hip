@@ -32,6 +32,7 @@ void set_pool_win(int v);
 void set_pool3_zg(int v);
 void set_pool_lds14(int v);
 void set_pw_res(int v);
+void set_pool3_g(int v);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out, int bn = 0);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
 hipError_t launch_conv3x3(int dtype, const uint16_t* in, const uint16_t* wpk, const float* bias, uint16_t* out,
@@ -1037,6 +1038,11 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "pool_roll") {  // MaxPool3d(3,1,1) on 7-wide maps: 1 (default) maxpool3_roll, k >= 2 k frames per thread, 0 maxpool3_s1; process-wide
     if (value < 0) return set_err(c, FAC_ERR_ARG, "pool_roll must be >= 0");
     fac::set_pool_roll(value);
+    return FAC_OK;
+  }
+  if (k == "pool3_g") {  // frames per maxpool3_pw unit on 7x7 maps: 0 default (2), 1, 2 or 4; process-wide
+    if (value != 0 && value != 1 && value != 2 && value != 4) return set_err(c, FAC_ERR_ARG, "pool3_g must be 0, 1, 2 or 4");
+    fac::set_pool3_g(value);
     return FAC_OK;
   }
   if (k == "pw_res") {  // 1 (default): ResNet's K = 128 / 256 conv3 + identity by pw_res; 0: convnd_pt; process-wide

@@ -883,10 +883,12 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
   int qoff[NIT], qinf[NIT];
 #pragma unroll
   for (int j = 0; j < NIT; ++j) {
-    const int q = tid + 256 * j, p = q >> 3, c8 = q & 7;
+    // (a non-item, q >= P * 8, points at its unit's first position: the
+    // branch-free loads below still read it, so it must be in the clip)
+    const int q = tid + 256 * j, item = q < P * 8, p = item ? q >> 3 : 0, c8 = q & 7;
     const int zz = p / (S * S), pos = p - zz * S * S, z = z0 + zz;
-    qoff[j] = z * fs + pos * C + c8 * 8;
-    qinf[j] = (p * 8 + (c8 ^ ((p >> 1) & 7))) * 8 | (q < P * 8 ? c8 : 8) << 16 | (z > 0) << 20 | (z + 1 < D) << 21;
+    qoff[j] = z * fs + pos * C + (item ? c8 * 8 : 0);
+    qinf[j] = (p * 8 + (c8 ^ ((p >> 1) & 7))) * 8 | (item ? c8 : 8) << 16 | (z > 0) << 20 | (z + 1 < D) << 21;
   }
   // phase 2 geometry: this lane's image row within a fragment row and column
   const int lr = r16 < RPT * S ? r16 / S : RPT - 1, x = r16 < RPT * S ? r16 - lr * S : S - 1;
@@ -913,37 +915,48 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
     for (int ct = 0; ct < CT; ++ct) acc[i][ct] = (f32x4)0.f;
 
   const int nch = kp / 64;
-  for (int kc = 0; kc < nch; ++kc) {
-    uint16_t* const img = tm + (kc & 1) * TMS;
-    const int kb = kc * 64, nval = min(8, (C - kb) >> 3);  // valid pieces of this chunk
-    uint16_t* const wimg = wl[kc & 1];
-#pragma unroll
-    for (int i = 0; i < WFW; ++i)
-      if (wave + 4 * i < 2 * CT) glds16(wsrc[i] + kb, wimg + (wave + 4 * i) * 512);
-    // 1. frame maxima into the image (pieces past C: zero, which the zero
-    // weight rows of k_pad multiply)
-    u32x4 v[NIT][3];
+  // chunk kc's pixel loads (pieces past C: zero, which the zero weight rows
+  // of k_pad multiply) and its weight fragments (glds); a chunk's loads are
+  // issued before the previous chunk's fragments and MFMAs, so each
+  // workgroup keeps one chunk in flight while it computes
+  u32x4 v[NIT][3];
+  // Branch-free: pieces past C (and non-items) load the chunk's first piece
+  // of the position, a valid address, and phase 1 zeroes them.
+  auto load = [&](int kc) __attribute__((always_inline)) {
+    const int kb = kc * 64, nval = min(8, (C - kb) >> 3);
 #pragma unroll
     for (int j = 0; j < NIT; ++j) {
-      if (((qinf[j] >> 16) & 15) < nval) {
-        const uint16_t* c = xb + qoff[j] + kb;
-        v[j][0] = *(const u32x4*)(c - ((qinf[j] >> 20) & 1) * fs);
-        v[j][1] = *(const u32x4*)c;
-        v[j][2] = *(const u32x4*)(c + ((qinf[j] >> 21) & 1) * fs);
-      } else {
-        v[j][0] = v[j][1] = v[j][2] = (u32x4)0u;
-      }
+      const int c8 = (qinf[j] >> 16) & 15;
+      const uint16_t* c = xb + qoff[j] + kb - (c8 < nval ? 0 : (c8 & 7) * 8);
+      v[j][0] = *(const u32x4*)(c - ((qinf[j] >> 20) & 1) * fs);
+      v[j][1] = *(const u32x4*)c;
+      v[j][2] = *(const u32x4*)(c + ((qinf[j] >> 21) & 1) * fs);
     }
 #pragma unroll
+    for (int i = 0; i < WFW; ++i)
+      if (wave + 4 * i < 2 * CT) glds16(wsrc[i] + kb, wl[kc & 1] + (wave + 4 * i) * 512);
+  };
+  load(0);
+  for (int kc = 0; kc < nch; ++kc) {
+    uint16_t* const img = tm + (kc & 1) * TMS;
+    const uint16_t* const wimg = wl[kc & 1];
+    // 1. frame maxima into the image.  (The empty asm pins the maxima here:
+    // computed right behind the prefetch, they would wait for its loads.)
+#pragma unroll
+    for (int j = 0; j < NIT; ++j) asm volatile("" : "+v"(v[j][0]), "+v"(v[j][1]), "+v"(v[j][2]));
+    const int nval = min(8, (C - kc * 64) >> 3);
+#pragma unroll
     for (int j = 0; j < NIT; ++j) {
-      if (((qinf[j] >> 16) & 15) >= 8) continue;
+      const int c8 = (qinf[j] >> 16) & 15;
+      if (c8 >= 8) continue;
       u32x4 m;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         m[i] = mp_max<T>(mp_max<T>(mp_key<T>(v[j][0][i]), mp_key<T>(v[j][1][i])), mp_key<T>(v[j][2][i]));
-      *(u32x4*)(img + (qinf[j] & 0xffff)) = m;
+      *(u32x4*)(img + (qinf[j] & 0xffff)) = c8 < nval ? m : (u32x4)0u;
     }
     __syncthreads();  // (its vmcnt(0) also lands the weight fragments)
+    if (kc + 1 < nch) load(kc + 1);  // its image / weight buffers were last read two chunks ago
     // 2 + 3. row and column maxima into B fragments, MFMAs
 #pragma unroll
     for (int i = 0; i < RTW; ++i) {
@@ -3257,6 +3270,10 @@ static int g_pool_lds14 = 1;
 // process-wide (fac_set_option "pw_res"): 1 (default) the K = 128 / 256
 // bottleneck conv3 + identity by pw_res, 0 by convnd_pt (A/B)
 static int g_pw_res = 1;
+// process-wide (fac_set_option "pool3_g"): frames per maxpool3_pw unit on
+// 7 x 7 maps, 0 = default (2), else 1 / 2 / 4 (A/B)
+static int g_pool3_g = 0;
+void set_pool3_g(int v) { g_pool3_g = v; }
 void set_pw_res(int v) { g_pw_res = v; }
 void set_pool_lds14(int v) { g_pool_lds14 = v; }
 
@@ -3439,7 +3456,10 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
         !(S == 14 || S == 7 || S == 3) || d->cout % 32 || d->ldo % 8 || d->c_off % 8)
       return FAC_ERR_ARG;
     // frames per unit: 196 positions at 7 x 7 when the clip allows, 18 at 3 x 3
-    const int G = S == 14 ? 1 : (S == 7 ? (d->d % 4 == 0 ? 4 : (d->d % 2 == 0 ? 2 : 1)) : (d->d % 2 == 0 ? 2 : 1));
+    // frames per unit at 7 x 7: 2 by default (98 positions; fac_set_option
+    // "pool3_g" 1 / 2 / 4 forces one where the clip allows), at 3 x 3: 2
+    const int g7 = g_pool3_g ? g_pool3_g : 2;
+    const int G = S == 14 ? 1 : (S == 7 ? (d->d % g7 == 0 ? g7 : (d->d % 2 == 0 ? 2 : 1)) : (d->d % 2 == 0 ? 2 : 1));
     const int nunits = d->n * (d->d / G);
     const int nct = d->cout % 64 == 0 ? 2 : 1;
     const dim3 grid((nunits + 7) / 8 * 8, d->cout / (32 * nct));
