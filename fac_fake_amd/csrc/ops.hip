@@ -2449,23 +2449,32 @@ __global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ i
 // for the fragment and residual reads: 16 rows of one piece column hit 16
 // distinct bank groups).  LDS: weights 64 KB + 2 x input tile + 2 x residual
 // tile = 160 KB for both instances.
-template <class T, int KC, int BN, int BM>
+// DUAL (layer1's first block, K = 64): no identity; a second 1x1 GEMM -- the
+// stride-1 downsample conv + bn over the block input x2 -- accumulates onto
+// relu(acc + b3) + b_ds (the reference's order, ResVitKan.py:146-152), both
+// weight blocks resident (2 x 32 KB), both inputs' tiles streamed (replaces
+// convnd_pt DUAL there, which ran this 7.4 GB / 0.63 TFLOP launch at 3.5 TB/s).
+template <class T, int KC, int BN, int BM, bool DUAL = false>
 __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
                                                  const float* __restrict__ bias, const uint16_t* __restrict__ res,
                                                  uint16_t* __restrict__ out, int M, int kp, int ldo, int c_off, int ldr,
-                                                 int r_off, int ny, int relu1, int relu2) {
+                                                 int r_off, int ny, int relu1, int relu2,
+                                                 const uint16_t* __restrict__ in2, const uint16_t* __restrict__ w2,
+                                                 const float* __restrict__ bias2) {
   constexpr int K = KC * 32, PPR = K / 8, RPR = BN / 8;  // 16-byte pieces per input / residual row
   constexpr int NW = 8, WN = BN / 64, WM = NW / WN, WPOS = BM / WM, PT = WPOS / 16;
-  constexpr int WEL = BN * K, AEL = BM * K, REL = BM * BN;  // elements
-  constexpr int APL = BM * PPR / 512, RPL = BM * RPR / 512;  // glds pieces per lane per tile
-  constexpr int SL = 2 * PT;                                 // 16-byte stores per lane per tile
-  static_assert(PT >= 1 && WPOS % 16 == 0 && APL * 512 == BM * PPR && RPL * 512 == BM * RPR, "tile shape");
-  static_assert(PPR >= 16 && RPR >= 16, "piece swizzle spans 16 slots");
-  static_assert(2 * (WEL + 2 * AEL + 2 * REL) <= 163840, "LDS");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[WEL + 2 * AEL + 2 * REL];
-  uint16_t* const sw = smem;
-  uint16_t* const sa = smem + WEL;
-  uint16_t* const sr = sa + 2 * AEL;
+  constexpr int NG = DUAL ? 2 : 1;                                // GEMMs (weight blocks, input tiles)
+  constexpr int WEL = BN * K, AEL = BM * K, REL = DUAL ? 0 : BM * BN;  // elements
+  constexpr int APL = BM * PPR / 512, RPL = DUAL ? 0 : BM * RPR / 512;  // glds pieces per lane per tile and GEMM
+  constexpr int SL = 2 * PT;                                            // 16-byte stores per lane per tile
+  constexpr int SWA = PPR >= 16 ? 15 : 7;                               // input-row piece swizzle mask
+  static_assert(PT >= 1 && WPOS % 16 == 0 && APL * 512 == BM * PPR && (DUAL || RPL * 512 == BM * RPR), "tile shape");
+  static_assert(PPR >= 8 && (DUAL || RPR >= 16), "piece swizzles");
+  static_assert(2 * (NG * WEL + 2 * NG * AEL + 2 * REL) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[NG * WEL + 2 * NG * AEL + 2 * REL];
+  uint16_t* const sw = smem;                 // [gemm][fragment]
+  uint16_t* const sa = smem + NG * WEL;      // [buf][gemm][BM][K]
+  uint16_t* const sr = sa + 2 * NG * AEL;    // [buf][BM][BN]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int wn = wave % WN, wm = wave / WN;
@@ -2478,25 +2487,33 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
   // the column block's weights, fragment (wn', k-step s, channel tile ct) as
   // a lane-ordered 1 KB image [g][r16][8]: row r16 of tile ct = channel
   // 32 (ct >> 1) + 8 (r16 >> 2) + 4 (ct & 1) + (r16 & 3) of group wn'
-  for (int f = wave; f < WN * KC * 4; f += NW) {
-    const int ct = f & 3, s = (f >> 2) % KC, wq = f / (4 * KC);
-    const int n = n0 + wq * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
-    *(u16x8*)(sw + f * 512 + lane * 8) = *(const u16x8*)(w + (size_t)n * kp + s * 32 + g * 8);
+#pragma unroll
+  for (int gi = 0; gi < NG; ++gi) {
+    const uint16_t* wg = gi ? w2 : w;
+    for (int f = wave; f < WN * KC * 4; f += NW) {
+      const int ct = f & 3, s = (f >> 2) % KC, wq = f / (4 * KC);
+      const int n = n0 + wq * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
+      *(u16x8*)(sw + gi * WEL + f * 512 + lane * 8) = *(const u16x8*)(wg + (size_t)n * kp + s * 32 + g * 8);
+    }
   }
-  float bv[2][8];
+  float bv[2][8], bv2[2][8];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bv[h][j] = bias ? bias[n0 + wn * 64 + 32 * h + 8 * g + j] : 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + wn * 64 + 32 * h + 8 * g + j;
+      bv[h][j] = bias ? bias[n] : 0.f;
+      bv2[h][j] = DUAL && bias2 ? bias2[n] : 0.f;
+    }
   // glds geometry: wave instruction i fills 64 consecutive 16-byte LDS units
   // q = (i NW + wave) 64 + lane of a tile image: row q / PR, slot q % PR,
-  // holding the row's piece slot ^ (row & 15)
-  int arow[APL], aoff[APL], rrow[RPL], roff[RPL];
+  // holding the row's piece slot ^ (row & mask)
+  int arow[APL], aoff[APL], rrow[RPL > 0 ? RPL : 1], roff[RPL > 0 ? RPL : 1];
 #pragma unroll
   for (int i = 0; i < APL; ++i) {
     const int q = (i * NW + wave) * 64 + lane, r = q / PPR, j = q - r * PPR;
     arow[i] = r;
-    aoff[i] = (j ^ (r & 15)) * 8;
+    aoff[i] = (j ^ (r & SWA)) * 8;
   }
 #pragma unroll
   for (int i = 0; i < RPL; ++i) {
@@ -2504,17 +2521,21 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
     rrow[i] = r;
     roff[i] = r_off + n0 + (j ^ (r & 15)) * 8;
   }
-  // a tile's input rows and residual block into buffer buf.  Rows past M
+  // a tile's input rows (and residual block) into buffer buf.  Rows past M
   // re-read row M - 1 (their outputs go to the sink) and tiles past the end
-  // re-read tile 0 into a buffer never read: every lane always issues APL +
-  // RPL pieces per tile from valid rows, branch-free, so the vmcnt counts
+  // re-read tile 0 into a buffer never read: every lane always issues the
+  // same pieces per tile from valid rows, branch-free, so the vmcnt counts
   // below hold
   auto issue = [&](int tile, int buf) {
     const int m0 = tile < nrt ? tile * BM : 0;
 #pragma unroll
-    for (int i = 0; i < APL; ++i) {
-      const int m = min(m0 + arow[i], M - 1);
-      glds16(in + (size_t)m * K + aoff[i], sa + buf * AEL + (i * NW + wave) * 64 * 8);
+    for (int gi = 0; gi < NG; ++gi) {
+      const uint16_t* src = gi ? in2 : in;
+#pragma unroll
+      for (int i = 0; i < APL; ++i) {
+        const int m = min(m0 + arow[i], M - 1);
+        glds16(src + (size_t)m * K + aoff[i], sa + (buf * NG + gi) * AEL + (i * NW + wave) * 64 * 8);
+      }
     }
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
@@ -2531,44 +2552,67 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
     if (it == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(SL) : "memory");
     issue(rt + rstep, buf ^ 1);  // its readers (the previous tile) passed the barrier
-    const uint16_t* a = sa + buf * AEL;
     f32x4 acc[PT][4];
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt)
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = (f32x4)0.f;
 #pragma unroll
-    for (int s = 0; s < KC; ++s) {
-      u16x8 wf[4];
+    for (int gi = 0; gi < NG; ++gi) {
+      if (gi == 1) {  // DUAL: conv3 done -> relu(acc + b3) + b_ds, the downsample accumulates on it
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) wf[ct] = *(const u16x8*)(sw + ((wn * KC + s) * 4 + ct) * 512 + lane * 8);
+        for (int pt = 0; pt < PT; ++pt)
 #pragma unroll
-      for (int pt = 0; pt < PT; ++pt) {
-        const int r = wm * WPOS + pt * 16 + r16;
-        const u16x8 pf = *(const u16x8*)(a + (r * PPR + ((s * 4 + g) ^ (r & 15))) * 8);
+          for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = T::mfma(wf[ct], pf, acc[pt][ct]);
+            for (int j = 0; j < 4; ++j) {
+              const int h = ct >> 1, e = ct & 1;
+              float x = acc[pt][ct][j] + bv[h][4 * e + j];
+              if (relu1) x = relu(x);
+              acc[pt][ct][j] = x + bv2[h][4 * e + j];
+            }
+      }
+      const uint16_t* a = sa + (buf * NG + gi) * AEL;
+      const uint16_t* wg = sw + gi * WEL;
+#pragma unroll
+      for (int s = 0; s < KC; ++s) {
+        u16x8 wf[4];
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) wf[ct] = *(const u16x8*)(wg + ((wn * KC + s) * 4 + ct) * 512 + lane * 8);
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) {
+          const int r = wm * WPOS + pt * 16 + r16;
+          const u16x8 pf = *(const u16x8*)(a + (r * PPR + ((s * 4 + g) ^ (r & SWA))) * 8);
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[pt][ct] = T::mfma(wf[ct], pf, acc[pt][ct]);
+        }
       }
     }
-    // epilogue: v = relu?(acc + b3) + residual, relu?; 16-byte stores of
-    // channels n0 + 64 wn + 32 h + 8 g .. +7
+    // epilogue: v = relu?(acc + b3) + residual, relu? (DUAL: relu?(acc));
+    // 16-byte stores of channels n0 + 64 wn + 32 h + 8 g .. +7
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) {
       const int r = wm * WPOS + pt * 16 + r16, m = rt * BM + r;
       uint16_t* o = m < M ? out + (size_t)m * ldo + c_off + n0 + wn * 64 + 8 * g : g_sink + lane * 8;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const u16x8 rv = *(const u16x8*)(sr + buf * REL + (r * RPR + ((wn * 8 + 4 * h + g) ^ (r & 15))) * 8);
+        u16x8 rv = (u16x8)0;
+        if constexpr (!DUAL) rv = *(const u16x8*)(sr + buf * REL + (r * RPR + ((wn * 8 + 4 * h + g) ^ (r & 15))) * 8);
         u16x4 q[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
           f32x4 v;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float x = acc[pt][2 * h + e][j] + bv[h][4 * e + j];
-            if (relu1) x = relu(x);
-            x += T::to_f32(rv[4 * e + j]);
-            if (relu2) x = relu(x);
+            float x = acc[pt][2 * h + e][j];
+            if constexpr (DUAL) {
+              if (relu2) x = relu(x);
+            } else {
+              x += bv[h][4 * e + j];
+              if (relu1) x = relu(x);
+              x += T::to_f32(rv[4 * e + j]);
+              if (relu2) x = relu(x);
+            }
             v[j] = x;
           }
           q[e] = T::pack4(v);
@@ -3521,7 +3565,8 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     uint16_t* o = (uint16_t*)d->out;
     const int mi = (int)M;
 #define FAC_PWR(TT, KC, BNN) \
-  pw_res<TT, KC, BNN, 64><<<G, 512, 0, st>>>(in, wt, d->bias, res, o, mi, k_pad, d->ldo, d->c_off, d->ldr, d->r_off, ny, r1, r2)
+  pw_res<TT, KC, BNN, 64><<<G, 512, 0, st>>>(in, wt, d->bias, res, o, mi, k_pad, d->ldo, d->c_off, d->ldr, d->r_off, ny, r1, r2, \
+                                             nullptr, nullptr, nullptr)
     if (d->dtype == FAC_DTYPE_BF16) {
       if (d->cin == 128) FAC_PWR(BF16, 4, 256);
       else FAC_PWR(BF16, 8, 128);
@@ -3807,6 +3852,22 @@ int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stre
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
     ncu = 256;
+  // layer1's first block (64 -> 256 twice, the downsample at stride 1 over
+  // the same positions): pw_res DUAL
+  if (g_pw_res && d->cin == 64 && ds->cin == 64 && d->cout % 256 == 0 && p.KD * p.KH * p.KW == 1 &&
+      q.KD * q.KH * q.KW == 1 && p.SD * p.SH * p.SW == 1 && q.SD * q.SH * q.SW == 1 && !p.PD && !p.PH && !p.PW &&
+      !q.PD && !q.PH && !q.PW && p.Kp == 64 && q.Kp == 64) {
+    const int ny2 = d->cout / 256, G2 = std::max(ny2, ncu / ny2 * ny2);
+    const int r1 = (d->flags & FAC_CONV_RELU) != 0, r2 = (d->flags & FAC_CONV_RELU2) != 0;
+    hipStream_t st2 = (hipStream_t)stream;
+#define FAC_PWD(TT)                                                                                                     \
+  pw_res<TT, 2, 256, 128, true><<<G2, 512, 0, st2>>>(p.in, p.w, p.bias, nullptr, (uint16_t*)p.out, p.M, 64, p.ldo,        \
+                                                      p.c_off, 0, 0, ny2, r1, r2, q.in, q.w, q.bias)
+    if (d->dtype == FAC_DTYPE_BF16) FAC_PWD(BF16);
+    else FAC_PWD(F16);
+#undef FAC_PWD
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
   // 128-wide tiles: the 256-wide DUAL variant needs 256+ VGPRs and spills
   // (scratch traffic would also break the hand-counted vmcnt waits)
   const int nrt = (p.M + 255) / 256, ny = p.Cout / 128;

@@ -327,7 +327,8 @@ def test_pw_res_bottleneck_conv3(n, h, w, cin, cout, dt):
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", [
     # (n, h, cin3, hx, cin_ds, stride_ds, cout): ResNet-50 bottleneck conv3 + downsample
-    (2, 56, 64, 56, 64, 1, 256),      # layer1 (two K steps: one per GEMM)
+    (2, 56, 64, 56, 64, 1, 256),      # layer1 (two K steps: one per GEMM; pw_res DUAL)
+    (3, 13, 64, 13, 64, 1, 256),      # layer1 shape class, 507 positions: a ragged last 128-row tile
     (2, 28, 128, 56, 256, 2, 512),    # layer2: strided downsample gather
     (2, 7, 512, 14, 1024, 2, 2048),   # layer4
     (3, 13, 128, 26, 256, 2, 128),    # ragged last row tile, one column block
