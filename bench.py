@@ -244,6 +244,8 @@ def layer_roofline_ms(run, dtype: str) -> dict:
         n, d, h, w, c = x.shape
         od, oh, ow = self.out_dims(d, h, w)
         M = n * od * oh * ow
+        if kw.get("prepool3s2"):   # pool + 1x1 (maxpool2s_pw): the pooled positions, the unpooled input read once
+            M = out.numel() // self.cout
         flops = 2.0 * M * self.cout * self.g.kd * self.g.kh * self.g.kw * self.cin
         esz = 4 if kw.get("out_f32") else 2
         byts = 2.0 * x.numel() + esz * M * self.cout + (2.0 * M * self.cout if kw.get("residual") is not None else 0)

@@ -1018,6 +1018,129 @@ __global__ __launch_bounds__(256, 2) void maxpool3_pw(const uint16_t* __restrict
   }
 }
 
+// ---- maxpool2s_pw (round 6): S3D's base.1 + base.2 -- MaxPool3d((1,3,3),
+// (1,2,2), (0,1,1)) then BasicConv3d(64, 64, 1) + BN + ReLU (model.py:19-20)
+// -- as one launch, so the pooled map is never written and read back (the
+// pool read 4.9 GB and wrote 1.2 GB at 1536 clips, the 1x1 read that 1.2 GB
+// again).  A unit is (clip, frame, RB pooled rows of a WO-wide map, i.e. the
+// 2 RB + 1 input rows under them):
+//  1. each (pooled row, input column, 16-byte piece) takes the max over its
+//     three input rows 2py-1 .. 2py+1 (three global loads, clamped: a max over
+//     a repeat) into an LDS image, piece c8 of column x at c8 ^ ((x >> 1) & 7);
+//  2. each wave forms its MFMA B fragments from the image: the max over input
+//     columns 2px-1 .. 2px+1 (three LDS reads, clamped), lane = pooled
+//     position;
+//  3. the 64 -> 64 conv's MFMAs from registers (weights glds'd to LDS as
+//     conv_pw's lane-ordered fragments), bias + ReLU, 16-byte stores.
+// Exact maxima on 16-bit patterns as in maxpool3_pw (mp_key / mp_max).
+template <class T, int WO, int RB>
+__global__ __launch_bounds__(256, 3) void maxpool2s_pw(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
+                                                       const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                       int nunits, int H, int Ho, int ldo, int c_off, int relu_on) {
+  constexpr int W = 2 * WO, C = 64, P = RB * WO;  // input row width, channels, pooled positions per unit
+  constexpr int NT = (P + 15) / 16, RTW = (NT + 3) / 4;
+  constexpr int NIT = (RB * W * 8 + 255) / 256;
+  constexpr int CT = 4;  // 64 output channels as 16-channel MFMA tiles
+  __shared__ __attribute__((aligned(16))) uint16_t img[RB * W * 64];
+  __shared__ __attribute__((aligned(16))) uint16_t wl[2 * CT * 512];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int per = (int)(gridDim.x >> 3);
+  const int u = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // contiguous units per XCD
+  if (u >= nunits) return;
+  const int nb = (Ho + RB - 1) / RB, fz = u / nb, py0 = (u - fz * nb) * RB;  // fz = clip * D + frame
+  const uint16_t* xb = in + (size_t)fz * H * W * C;
+  // weights: fragment f = s * CT + ct by wave f % 4 (conv_pw's channel order)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int f = wave + 4 * i, ct = f % CT, s = f / CT;
+    glds16(w + (size_t)(32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3)) * 64 + s * 32 + g * 8,
+           wl + f * 512);
+  }
+  // 1. row maxima: item (pooled row r, input column x, piece c8)
+  u32x4 v[NIT][3];
+  int slot[NIT];
+#pragma unroll
+  for (int j = 0; j < NIT; ++j) {
+    const int q = tid + 256 * j, c8 = q & 7, x = (q >> 3) % W, r = (q >> 3) / W;
+    const int py = min(py0 + r, Ho - 1), y1 = 2 * py;
+    const int y0 = max(y1 - 1, 0), y2 = min(y1 + 1, H - 1);
+    const uint16_t* c = xb + (size_t)x * C + c8 * 8;
+    v[j][0] = *(const u32x4*)(c + (size_t)y0 * W * C);
+    v[j][1] = *(const u32x4*)(c + (size_t)y1 * W * C);
+    v[j][2] = *(const u32x4*)(c + (size_t)y2 * W * C);
+    slot[j] = ((r * W + x) * 8 + (c8 ^ ((x >> 1) & 7))) * 8;
+  }
+  // every item is real (no branch here: a guarded use let the compiler sink
+  // the loads of the guarded items behind the first maxima, a round trip each)
+  static_assert(NIT * 256 == RB * W * 8, "whole items per thread");
+  __builtin_amdgcn_sched_barrier(0);  // all 3 NIT loads issued before the first maximum
+#pragma unroll
+  for (int j = 0; j < NIT; ++j) {
+    u32x4 m;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      m[i] = mp_max<T>(mp_max<T>(mp_key<T>(v[j][0][i]), mp_key<T>(v[j][1][i])), mp_key<T>(v[j][2][i]));
+    *(u32x4*)(img + slot[j]) = m;
+  }
+  __syncthreads();
+  // 2 + 3. column maxima into B fragments, MFMAs
+  f32x4 acc[RTW][CT];
+#pragma unroll
+  for (int i = 0; i < RTW; ++i)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[i][ct] = (f32x4)0.f;
+#pragma unroll
+  for (int i = 0; i < RTW; ++i) {
+    const int t = wave + 4 * i;
+    if (t >= NT) break;
+    const int p = min(t * 16 + r16, P - 1), r = p / WO, px = p - r * WO;
+    const int x1 = 2 * px, x0 = max(x1 - 1, 0), x2 = min(x1 + 1, W - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c8 = s * 4 + g;
+      const u32x4 a = *(const u32x4*)(img + ((r * W + x0) * 8 + (c8 ^ ((x0 >> 1) & 7))) * 8);
+      const u32x4 b = *(const u32x4*)(img + ((r * W + x1) * 8 + (c8 ^ ((x1 >> 1) & 7))) * 8);
+      const u32x4 c = *(const u32x4*)(img + ((r * W + x2) * 8 + (c8 ^ ((x2 >> 1) & 7))) * 8);
+      const u32x4 vm = mp_max4<T>(mp_max4<T>(a, b), c);
+      u32x4 f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) f[e] = mp_key<T>(vm[e]);
+      const u16x8 pf = __builtin_bit_cast(u16x8, f);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[i][ct] = T::mfma(*(const u16x8*)(wl + (s * CT + ct) * 512 + lane * 8), pf, acc[i][ct]);
+    }
+  }
+  // epilogue: bias + ReLU, 16-byte stores of channels 32 h + 8 g .. + 7
+  float bv[CT][4];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[ct][j] = bias ? bias[32 * (ct >> 1) + 8 * g + 4 * (ct & 1) + j] : 0.f;
+#pragma unroll
+  for (int i = 0; i < RTW; ++i) {
+    const int t = wave + 4 * i, p = t * 16 + r16, r = p / WO, px = p - r * WO;
+    if (t >= NT) break;
+    if (p >= P || py0 + r >= Ho) continue;
+    uint16_t* o = out + ((size_t)fz * Ho * WO + (size_t)(py0 + r) * WO + px) * ldo + c_off + 8 * g;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u16x4 q[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        f32x4 vv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float z = acc[i][2 * h + e][j] + bv[2 * h + e][j];
+          vv[j] = relu_on ? relu(z) : z;
+        }
+        q[e] = T::pack4(vv);
+      }
+      *(u16x8*)(o + 32 * h) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+}
+
 // ---- input staging
 template <class T, bool U8>
 __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
@@ -3411,6 +3534,29 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
   if (!d || !d->in || !d->weight || !d->out) return FAC_ERR_ARG;
   if (d->dtype != FAC_DTYPE_BF16 && d->dtype != FAC_DTYPE_F16) return FAC_ERR_ARG;
   if (d->cin <= 0 || d->cin % 8 || d->cout <= 0 || d->n <= 0 || d->d <= 0 || d->h <= 0 || d->w <= 0) return FAC_ERR_SHAPE;
+  // MaxPool3d((1,3,3), (1,2,2), (0,1,1)) over the input, then this 1x1x1
+  // 64 -> 64 conv (S3D's base.1 + base.2): maxpool2s_pw
+  if (d->flags & FAC_CONV_PREPOOL3S2) {
+    if ((d->flags & ~(FAC_CONV_RELU | FAC_CONV_PREPOOL3S2)) || out1 || out2 || d->kd != 1 || d->kh != 1 ||
+        d->kw != 1 || d->sd != 1 || d->sh != 1 || d->sw != 1 || d->pd || d->ph || d->pw || d->cin != 64 ||
+        d->cout != 64 || d->w != 56 || d->k_pad != 64 || d->od != d->d || d->oh != (d->h - 1) / 2 + 1 ||
+        d->ow != 28 || d->ldo % 8 || d->c_off % 8 || d->ldo < d->c_off + 64)
+      return FAC_ERR_ARG;
+    constexpr int RB = 4;
+    const int nunits = d->n * d->d * ((d->oh + RB - 1) / RB);
+    const int grid = (nunits + 7) / 8 * 8;
+    hipStream_t st = (hipStream_t)stream;
+    const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
+    if (d->dtype == FAC_DTYPE_BF16)
+      fac::maxpool2s_pw<fac::BF16, 28, RB><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight,
+                                                                 d->bias, (uint16_t*)d->out, nunits, d->h, d->oh,
+                                                                 d->ldo, d->c_off, relu_on);
+    else
+      fac::maxpool2s_pw<fac::F16, 28, RB><<<grid, 256, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight,
+                                                                d->bias, (uint16_t*)d->out, nunits, d->h, d->oh,
+                                                                d->ldo, d->c_off, relu_on);
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
   if (d->kd <= 0 || d->kh <= 0 || d->kw <= 0 || d->sd <= 0 || d->sh <= 0 || d->sw <= 0) return FAC_ERR_SHAPE;
   if (d->pd < 0 || d->ph < 0 || d->pw < 0 || d->od <= 0 || d->oh <= 0 || d->ow <= 0) return FAC_ERR_SHAPE;
   // output dims must be the floor-mode ones (every gathered tap then stays

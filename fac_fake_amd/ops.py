@@ -18,7 +18,7 @@ from . import _lib
 
 TORCH16 = {"bf16": torch.bfloat16, "fp16": torch.float16}
 
-RELU, RESID, RELU2, OUT_F32, MAXPOOL3S2, MAXPOOL3S1 = 1, 2, 4, 8, 16, 32   # FAC_CONV_* flags
+RELU, RESID, RELU2, OUT_F32, MAXPOOL3S2, MAXPOOL3S1, PREPOOL3S2 = 1, 2, 4, 8, 16, 32, 64   # FAC_CONV_* flags
 
 
 class ConvDesc(ctypes.Structure):
@@ -185,6 +185,15 @@ class ConvLayer:
                 and h == w and h in self.MAXPOOL3S1_MAPS and self.cout % 32 == 0 and c_off % 8 == 0
                 and (out is None or out.shape[4] % 8 == 0) and _lib.exports("fac_conv_nd"))
 
+    def prepool3s2_ok(self, x: torch.Tensor) -> bool:
+        """Whether fac_conv_nd takes FAC_CONV_PREPOOL3S2 for this layer on x:
+        MaxPool3d((1,3,3), (1,2,2), (0,1,1)) of x, then this 1x1x1 64 -> 64
+        conv (S3D's base.1 + base.2 at 112^2 clips, ops.hip maxpool2s_pw)."""
+        g = self.g
+        return ((g.kd, g.kh, g.kw, g.sd, g.sh, g.sw, g.pd, g.ph, g.pw) == (1, 1, 1, 1, 1, 1, 0, 0, 0)
+                and self.cin == 64 and self.cin_p == 64 and self.cout == 64 and x.shape[3] == 56
+                and x.shape[4] == 64)
+
     def out_dims(self, d, h, w):
         g = self.g
         return ((d + 2 * g.pd - g.kd) // g.sd + 1, (h + 2 * g.ph - g.kh) // g.sh + 1,
@@ -192,17 +201,25 @@ class ConvLayer:
 
     def __call__(self, x: torch.Tensor, *, relu: bool = True, out: torch.Tensor | None = None, c_off: int = 0,
                  residual: torch.Tensor | None = None, relu2: bool = False, out_f32: bool = False,
-                 maxpool3s2: bool = False, maxpool3s1: bool = False) -> torch.Tensor:
+                 maxpool3s2: bool = False, maxpool3s1: bool = False, prepool3s2: bool = False) -> torch.Tensor:
         """maxpool3s2: MaxPool2d(3, 2, 1) over H, W fused into the launch
         (FAC_CONV_MAXPOOL3S2: the space-to-depth first conv with relu only;
         the output is the pooled [N, D, Ho/2, Wo/2, C]).  maxpool3s1:
         MaxPool3d(3, 1, 1) over the INPUT first (FAC_CONV_MAXPOOL3S1: a 1x1x1
-        conv on a 14 / 7 / 3 square map, cout % 32 == 0; maxpool3s1_ok)."""
+        conv on a 14 / 7 / 3 square map, cout % 32 == 0; maxpool3s1_ok).
+        prepool3s2: MaxPool3d((1,3,3), (1,2,2), (0,1,1)) over the INPUT
+        first, the output at the pooled positions (FAC_CONV_PREPOOL3S2:
+        prepool3s2_ok)."""
         n, d, h, w, c = x.shape
         if c != self.cin_p or x.dtype != TORCH16[self.dtype] or not x.is_contiguous():
             raise ValueError(f"conv input must be contiguous {self.dtype} [N,D,H,W,{self.cin_p}], got "
                              f"{x.dtype} {tuple(x.shape)}")
         od, oh, ow = self.out_dims(d, h, w)
+        if prepool3s2:
+            if not self.prepool3s2_ok(x) or residual is not None or relu2 or out_f32 or maxpool3s2 or maxpool3s1:
+                raise ValueError("prepool3s2 needs a 1x1x1 64 -> 64 conv on a 56-wide map, no residual / relu2 / "
+                                 "fp32 output / other pool")
+            oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
         if maxpool3s2:
             if not relu or residual is not None or relu2 or out_f32 or c_off or oh % 2 or ow % 2:
                 raise ValueError("maxpool3s2 needs relu, no residual / relu2 / fp32 output, even output dims")
@@ -216,7 +233,7 @@ class ConvLayer:
             raise ValueError("maxpool3s1 needs a 1x1x1 conv over a 14 / 7 / 3 square map, cout % 32 == 0, "
                              "no residual / relu2 / fp32 output, ldo and c_off % 8 == 0")
         if (self._w33 is not None and h == w and residual is None and not relu2 and not out_f32 and c_off == 0
-                and not maxpool3s2 and not maxpool3s1 and out.shape[4] == self.cout and self.cin_p == self.cin):
+                and not maxpool3s2 and not maxpool3s1 and not prepool3s2 and out.shape[4] == self.cout and self.cin_p == self.cin):
             pk = self._packed33(h)
             if pk is not None:
                 lib = _lib.load()
@@ -236,7 +253,8 @@ class ConvLayer:
         dsc.od, dsc.oh, dsc.ow = (od, 2 * oh, 2 * ow) if maxpool3s2 else (od, oh, ow)
         dsc.out, dsc.ldo, dsc.c_off = out.data_ptr(), out.shape[4], c_off
         flags = (RELU if relu else 0) | (RELU2 if relu2 else 0) | (OUT_F32 if out_f32 else 0) | \
-            (MAXPOOL3S2 if maxpool3s2 else 0) | (MAXPOOL3S1 if maxpool3s1 else 0)
+            (MAXPOOL3S2 if maxpool3s2 else 0) | (MAXPOOL3S1 if maxpool3s1 else 0) | \
+            (PREPOOL3S2 if prepool3s2 else 0)
         if residual is not None:
             if tuple(residual.shape[:4]) != (n, od, oh, ow) or residual.dtype != x.dtype:
                 raise ValueError("residual must match the output positions and dtype")

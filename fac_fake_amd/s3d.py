@@ -200,6 +200,9 @@ class S3D(nn.Module):
     # branch3's MaxPool3d(3, 1, 1) fused into its 1x1x1 conv (FAC_CONV_MAXPOOL3S1)
     # on the 14 / 7 / 3 maps; False: fac_pool_nd then the conv (A/B)
     fuse_pool3 = True
+    # base.1's pool fused into base.2's 1x1x1 conv (FAC_CONV_PREPOOL3S2) on
+    # 56-wide maps; False: fac_pool_nd then the conv (A/B)
+    fuse_pool1 = True
 
     def _pad64(self, c: int, level: int) -> int:
         if self.pad64_level < level or c % 64 == 0 or (level == 1 and c < 64):
@@ -253,7 +256,19 @@ class S3D(nn.Module):
             n, d, h, w, _ = y.shape
             s = torch.zeros(n, d, h, w, 32, dtype=y.dtype, device=y.device)   # 30 filters + 2 zero channels
             y = self._srm_conv(y, relu=False, out=s)
-        for kind, L in self._layers:
+        skip = False
+        for li, (kind, L) in enumerate(self._layers):
+            if skip:   # base.2, run with base.1's pool below
+                skip = False
+                continue
+            nxt = self._layers[li + 1] if li + 1 < len(self._layers) else (None, None)
+            if (kind == "pool" and self.fuse_pool1 and L == ((1, 3, 3), (1, 2, 2), (0, 1, 1)) and nxt[0] == "basic"
+                    and taps is None and nxt[1].prepool3s2_ok(y)):   # (taps: base.1's own output is one)
+                # base.1's MaxPool3d((1,3,3),(1,2,2)) + base.2's 1x1x1 conv as one
+                # launch (FAC_CONV_PREPOOL3S2, ops.hip maxpool2s_pw)
+                y = nxt[1](y, prepool3s2=True)
+                skip = True
+                continue
             if kind == "sep_s2d":
                 # the raw clip (`_pack`): the space-to-depth packing runs
                 # inside the conv's halo staging (ops.conv_s2d4_clip); packed

@@ -34,6 +34,15 @@ extern "C" {
                                 first conv below (ResNet-50's conv1 + bn1 +
                                 relu + maxpool, ResVitKan.py:187/205);
                                 FAC_ERR_ARG otherwise */
+#define FAC_CONV_PREPOOL3S2 64 /* MaxPool3d((1,3,3), (1,2,2), (0,1,1)) over the
+                                INPUT first, then the conv: a 1x1x1 conv,
+                                cin = cout = 64, input width 56 (rows of
+                                28 pooled positions); desc->d/h/w are the
+                                unpooled input's, od/oh/ow the pooled
+                                output's; flags FAC_CONV_RELU at most besides
+                                this one; FAC_ERR_ARG otherwise.  S3D's
+                                base.1 + base.2 (model.py:19-20) without
+                                the pooled map in memory */
 #define FAC_CONV_MAXPOOL3S1 32 /* MaxPool3d(3, 1, 1) over the INPUT first
                                 (-inf padding), then the conv: a 1x1x1 conv
                                 (stride 1, no padding) over an S x S map,

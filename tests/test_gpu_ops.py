@@ -524,6 +524,39 @@ def test_conv_maxpool3s1_fused(n, d, h, cin, cout, c_off, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("n,d,h,c_off", [(2, 8, 56, 0), (3, 2, 30, 8), (1, 3, 9, 16)])
+def test_conv_prepool3s2_fused(n, d, h, c_off, dt):
+    """FAC_CONV_PREPOOL3S2 (ops.hip maxpool2s_pw): S3D's base.1 + base.2,
+    MaxPool3d((1,3,3), (1,2,2), (0,1,1)) then a 1x1x1 64 -> 64 conv + bias +
+    ReLU in one launch, on 56-wide maps of 56 / 30 / 9 rows (the last band of
+    4 pooled rows partial for 30 and 9), into a channel slot: against PyTorch
+    fp32 of the same 16-bit operands within one 16-bit ulp, against
+    fac_pool_nd + the conv's own kernel within one ulp, the neighbouring
+    channels untouched.  Inputs of both signs."""
+    from fac_fake_amd.ops import ConvLayer, pool
+    g = torch.Generator().manual_seed(41 + d + h)
+    x = torch.randn(n, 64, d, h, 56, generator=g).to(T16[dt]).float()
+    wt = torch.randn(64, 64, 1, 1, 1, generator=g) / 8.0
+    b = torch.randn(64, generator=g) * 0.1
+    layer = ConvLayer(wt, b, 1, 0, dtype=dt, device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    assert layer.prepool3s2_ok(xg)
+    ho = (h - 1) // 2 + 1
+    big = torch.full((n, d, ho, 28, 64 + 24), 5.0, dtype=T16[dt], device=DEV)
+    layer(xg, relu=True, out=big, c_off=c_off, prepool3s2=True)
+    unf = layer(pool(xg, (1, 3, 3), (1, 2, 2), (0, 1, 1), "max"), relu=True)
+    torch.cuda.synchronize()
+    pooled = F.max_pool3d(x, (1, 3, 3), (1, 2, 2), (0, 1, 1))
+    ref = F.relu(F.conv3d(pooled, wt.to(T16[dt]).float(), b)).permute(0, 2, 3, 4, 1).to(T16[dt])
+    bc = big.cpu()
+    got = bc[..., c_off:c_off + 64]
+    u = _ulps(got, ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05, float(u.max())
+    assert _ulps(got, unf.cpu(), dt).max() <= 1.0
+    assert torch.all(bc[..., :c_off] == 5.0) and torch.all(bc[..., c_off + 64:] == 5.0)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("h,w,pb,pa", [(30, 26, 2, 1), (224, 224, 2, 1), (18, 16, 0, 0)])
 def test_pack_input_s2d_u8_cells(h, w, pb, pa, dt):
     """fac_pack_input_s2d on uint8 NHWC images (ResNet-50's conv1 input,

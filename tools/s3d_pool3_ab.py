@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--attr", default="fuse_pool3", choices=["fuse_pool3", "fuse_pool1"],
+                    help="the S3D switch the arms toggle (branch3's pool, or base.1's)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     m = S3D(1, "no", dtype=a.dtype)
@@ -35,7 +37,7 @@ def main():
     graphs, outs = {}, {}
     with torch.cuda.stream(s):
         for arm in (True, False):
-            m.fuse_pool3 = arm
+            setattr(m, a.attr, arm)
             m(x)
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
@@ -46,7 +48,7 @@ def main():
             g.replay()
         torch.cuda.synchronize(dev)
         d = (outs[True].float() - outs[False].float()).abs().max().item()
-        print(f"B={a.B} {a.dtype}: max |logit fused - unfused| = {d:.3e}", flush=True)
+        print(f"{a.attr} B={a.B} {a.dtype}: max |logit fused - unfused| = {d:.3e}", flush=True)
         for r in range(a.rounds):
             for arm in (True, False):
                 g = graphs[arm]
