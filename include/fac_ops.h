@@ -76,8 +76,10 @@ extern "C" {
  * ResNet-50's / S3D's first conv) and temporal (kd,1,1) convs with 8 output
  * frames, cin % 64 == 0, cout % 64 == 0 (conv_tk), and
  * stride-1 1x1 convs with cin 64, 128 or 256, cout % 64 == 0, no fp32
- * output (conv_pw: ResNet-50's K <= 256 bottleneck 1x1s).  FAC_CONV_PW=0 in the
- * environment keeps the latter on the generic kernel. */
+ * output (conv_pw: ResNet-50's K <= 256 bottleneck 1x1s), of which the
+ * residual ones with cin 128 (cout % 256 == 0) or 256 (cout % 128 == 0) take
+ * pw_res (ResNet-50 layer2 / layer3 conv3 + identity; fac_set_option
+ * "pw_res" 0 routes them to the generic kernel for A/B). */
 typedef struct fac_conv_desc {
   int dtype;
   const void* in;
@@ -115,7 +117,9 @@ int fac_conv_nd_split(const fac_conv_desc* desc, void* out1, int ldo1, int split
  * output never goes through memory.  Both convs: cin % 64 == 0, the same
  * output positions [n, od, oh, ow] and cout (% 128 == 0); ds->out is ignored
  * and ds->flags must be 0; no FAC_CONV_RESID / FAC_CONV_OUT_F32 on desc.
- * Replaces fac_conv_nd(ds) + fac_conv_nd(desc with residual = its output). */
+ * Replaces fac_conv_nd(ds) + fac_conv_nd(desc with residual = its output).
+ * Layer1's 64 -> 256 pair with a stride-1 1x1 downsample runs on pw_res
+ * DUAL (both weight blocks resident in LDS), the others on convnd_pt DUAL. */
 int fac_conv_nd_dual(const fac_conv_desc* desc, const fac_conv_desc* ds, void* stream);
 
 /* A ResNet-50 layer1 / layer2 bottleneck's conv3 and the next block's conv1
