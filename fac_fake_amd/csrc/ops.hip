@@ -2577,22 +2577,28 @@ __global__ __launch_bounds__(256, 3) void conv_pw(const uint16_t* __restrict__ i
 // relu(acc + b3) + b_ds (the reference's order, ResVitKan.py:146-152), both
 // weight blocks resident (2 x 32 KB), both inputs' tiles streamed (replaces
 // convnd_pt DUAL there, which ran this 7.4 GB / 0.63 TFLOP launch at 3.5 TB/s).
-template <class T, int KC, int BN, int BM, bool DUAL = false>
+// PLAIN (MODE 2: S3D's merged Inception heads at 14 x 14, K = 192 / 256): no
+// identity, relu?(acc + b) into up to three column segments (out / out1 /
+// out2, fac_conv_nd_split); channels past cout (the zero-padded block tail)
+// store to the sink.
+template <class T, int KC, int BN, int BM, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
                                                  const float* __restrict__ bias, const uint16_t* __restrict__ res,
                                                  uint16_t* __restrict__ out, int M, int kp, int ldo, int c_off, int ldr,
                                                  int r_off, int ny, int relu1, int relu2,
                                                  const uint16_t* __restrict__ in2, const uint16_t* __restrict__ w2,
-                                                 const float* __restrict__ bias2) {
+                                                 const float* __restrict__ bias2, int cout, uint16_t* __restrict__ out1,
+                                                 int ldo1, int split1, uint16_t* __restrict__ out2, int ldo2, int split2) {
+  constexpr bool DUAL = MODE == 1, RESM = MODE == 0;
   constexpr int K = KC * 32, PPR = K / 8, RPR = BN / 8;  // 16-byte pieces per input / residual row
   constexpr int NW = 8, WN = BN / 64, WM = NW / WN, WPOS = BM / WM, PT = WPOS / 16;
   constexpr int NG = DUAL ? 2 : 1;                                // GEMMs (weight blocks, input tiles)
-  constexpr int WEL = BN * K, AEL = BM * K, REL = DUAL ? 0 : BM * BN;  // elements
-  constexpr int APL = BM * PPR / 512, RPL = DUAL ? 0 : BM * RPR / 512;  // glds pieces per lane per tile and GEMM
+  constexpr int WEL = BN * K, AEL = BM * K, REL = RESM ? BM * BN : 0;  // elements
+  constexpr int APL = BM * PPR / 512, RPL = RESM ? BM * RPR / 512 : 0;  // glds pieces per lane per tile and GEMM
   constexpr int SL = 2 * PT;                                            // 16-byte stores per lane per tile
-  constexpr int SWA = PPR >= 16 ? 15 : 7;                               // input-row piece swizzle mask
-  static_assert(PT >= 1 && WPOS % 16 == 0 && APL * 512 == BM * PPR && (DUAL || RPL * 512 == BM * RPR), "tile shape");
-  static_assert(PPR >= 8 && (DUAL || RPR >= 16), "piece swizzles");
+  constexpr int SWA = PPR % 16 == 0 ? 15 : 7;                           // input-row piece swizzle mask (stays in the row)
+  static_assert(PT >= 1 && WPOS % 16 == 0 && APL * 512 == BM * PPR && (!RESM || RPL * 512 == BM * RPR), "tile shape");
+  static_assert(PPR % 8 == 0 && (!RESM || RPR >= 16), "piece swizzles");
   static_assert(2 * (NG * WEL + 2 * NG * AEL + 2 * REL) <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) uint16_t smem[NG * WEL + 2 * NG * AEL + 2 * REL];
   uint16_t* const sw = smem;                 // [gemm][fragment]
@@ -2720,7 +2726,7 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         u16x8 rv = (u16x8)0;
-        if constexpr (!DUAL) rv = *(const u16x8*)(sr + buf * REL + (r * RPR + ((wn * 8 + 4 * h + g) ^ (r & 15))) * 8);
+        if constexpr (RESM) rv = *(const u16x8*)(sr + buf * REL + (r * RPR + ((wn * 8 + 4 * h + g) ^ (r & 15))) * 8);
         u16x4 q[2];
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -2730,6 +2736,9 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
             float x = acc[pt][2 * h + e][j];
             if constexpr (DUAL) {
               if (relu2) x = relu(x);
+            } else if constexpr (MODE == 2) {
+              x += bv[h][4 * e + j];
+              if (relu1) x = relu(x);
             } else {
               x += bv[h][4 * e + j];
               if (relu1) x = relu(x);
@@ -2740,7 +2749,15 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
           }
           q[e] = T::pack4(v);
         }
-        *(u16x8*)(m < M ? o + 32 * h : o) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+        uint16_t* dst = m < M ? o + 32 * h : o;
+        if constexpr (MODE == 2) {  // column segments (8-aligned: a lane's 8 channels never straddle one)
+          const int cg = n0 + wn * 64 + 32 * h + 8 * g;
+          dst = m >= M || cg >= cout ? g_sink + lane * 8
+                : cg >= split2     ? out2 + (size_t)m * ldo2 + (cg - split2)
+                : cg >= split1     ? out1 + (size_t)m * ldo1 + (cg - split1)
+                                   : dst;
+        }
+        *(u16x8*)dst = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
       }
     }
   }
@@ -3694,6 +3711,32 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
                                            (uint16_t*)d->out, nbox, d->h, d->w, d->oh, d->ow, k_pad, relu_on);
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
+  // S3D's merged Inception heads at K = 192 / 256 (fac_conv_nd_split, 1x1,
+  // relu(conv + b) into up to three column segments): pw_res PLAIN, 128-wide
+  // column blocks over the zero-padded weight rows
+  if (g_pw_res && split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
+      d->pd == 0 && d->ph == 0 && d->pw == 0 && !(d->flags & ~FAC_CONV_RELU) && k_pad == d->cin &&
+      (d->cin == 192 || d->cin == 256) && d->ldo % 8 == 0 && d->c_off % 8 == 0 && ldo1 % 8 == 0 && ldo2 % 8 == 0 &&
+      split1 % 8 == 0 && (split2 == INT_MAX || split2 % 8 == 0) && cout_pad % 128 == 0) {
+    const int ny = cout_pad / 128, ncu = cu_count();
+    const int G = std::max(ny, ncu / ny * ny);
+    const int r1 = (d->flags & FAC_CONV_RELU) != 0;
+    const uint16_t* in = (const uint16_t*)d->in;
+    const uint16_t* wt = (const uint16_t*)d->weight;
+#define FAC_PWS(TT, KC)                                                                                              \
+  pw_res<TT, KC, 128, 64, 2><<<G, 512, 0, st>>>(in, wt, d->bias, nullptr, (uint16_t*)d->out, (int)M, k_pad, d->ldo, \
+                                                d->c_off, 0, 0, ny, r1, 0, nullptr, nullptr, nullptr, d->cout,      \
+                                                (uint16_t*)out1, ldo1, split1, (uint16_t*)out2, ldo2, split2)
+    if (d->dtype == FAC_DTYPE_BF16) {
+      if (d->cin == 192) FAC_PWS(BF16, 6);
+      else FAC_PWS(BF16, 8);
+    } else {
+      if (d->cin == 192) FAC_PWS(F16, 6);
+      else FAC_PWS(F16, 8);
+    }
+#undef FAC_PWS
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
   // the bottleneck conv3 + identity at K = 128 / 256 (ResNet-50 layer2 /
   // layer3, relu(relu(conv + b) + residual)): pw_res
   if (g_pw_res && !split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 && d->sw == 1 &&
@@ -3712,7 +3755,7 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     const int mi = (int)M;
 #define FAC_PWR(TT, KC, BNN) \
   pw_res<TT, KC, BNN, 64><<<G, 512, 0, st>>>(in, wt, d->bias, res, o, mi, k_pad, d->ldo, d->c_off, d->ldr, d->r_off, ny, r1, r2, \
-                                             nullptr, nullptr, nullptr)
+                                             nullptr, nullptr, nullptr, INT_MAX, nullptr, 0, INT_MAX, nullptr, 0, INT_MAX)
     if (d->dtype == FAC_DTYPE_BF16) {
       if (d->cin == 128) FAC_PWR(BF16, 4, 256);
       else FAC_PWR(BF16, 8, 128);
@@ -4007,8 +4050,9 @@ int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stre
     const int r1 = (d->flags & FAC_CONV_RELU) != 0, r2 = (d->flags & FAC_CONV_RELU2) != 0;
     hipStream_t st2 = (hipStream_t)stream;
 #define FAC_PWD(TT)                                                                                                     \
-  pw_res<TT, 2, 256, 128, true><<<G2, 512, 0, st2>>>(p.in, p.w, p.bias, nullptr, (uint16_t*)p.out, p.M, 64, p.ldo,        \
-                                                      p.c_off, 0, 0, ny2, r1, r2, q.in, q.w, q.bias)
+  pw_res<TT, 2, 256, 128, 1><<<G2, 512, 0, st2>>>(p.in, p.w, p.bias, nullptr, (uint16_t*)p.out, p.M, 64, p.ldo,           \
+                                                   p.c_off, 0, 0, ny2, r1, r2, q.in, q.w, q.bias, INT_MAX, nullptr, 0, INT_MAX, \
+                                                   nullptr, 0, INT_MAX)
     if (d->dtype == FAC_DTYPE_BF16) FAC_PWD(BF16);
     else FAC_PWD(F16);
 #undef FAC_PWD

@@ -857,6 +857,43 @@ def test_conv_split_equals_separate_convs(dt, pt_wide, shape):
         _nd_pt_wide(32, dt)
 
 
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("shape,cin,widths", [
+    ((3, 8, 14, 14), 192, (64, 96, 16)),     # Mixed_3b's heads: 176 columns = two 128-wide blocks, ragged rows
+    ((3, 8, 14, 14), 256, (128, 128, 32)),   # Mixed_3c's heads: 288 = three blocks, the last a quarter full
+    ((1, 1, 5, 7), 256, (64, 96, 16)),       # fewer row tiles than workgroups
+])
+def test_pw_res_split_heads(shape, cin, widths, dt):
+    """fac_conv_nd_split at K = 192 / 256 on pw_res PLAIN (S3D's merged
+    Inception heads at 14 x 14: weights resident in LDS, input rows streamed):
+    each column segment within one 16-bit ulp of its own fac_conv_nd launch
+    (other kernels, other summation order) and of PyTorch fp32 on the same
+    operands, the rest of the concat buffer untouched."""
+    from fac_fake_amd.ops import ConvLayer, conv_split
+    g = torch.Generator().manual_seed(13 + cin)
+    n, d, h, w = shape
+    x = torch.randn(n, d, h, w, cin, generator=g).to(T16[dt])
+    ws = [torch.randn(c, cin, 1, 1, 1, generator=g) / np.sqrt(cin) for c in widths]
+    bs = [torch.randn(c, generator=g) * 0.1 for c in widths]
+    sep = [ConvLayer(wi, bi, 1, 0, dtype=dt, device=DEV) for wi, bi in zip(ws, bs)]
+    merged = ConvLayer(torch.cat(ws), torch.cat(bs), 1, 0, dtype=dt, device=DEV)
+    xg = x.to(DEV)
+    out = torch.zeros(n, d, h, w, 512, dtype=T16[dt], device=DEV)
+    h1 = torch.empty(n, d, h, w, widths[1], dtype=T16[dt], device=DEV)
+    h2 = torch.empty(n, d, h, w, widths[2], dtype=T16[dt], device=DEV)
+    conv_split(merged, xg, (widths[0], widths[0] + widths[1]), out, 0, h1, h2)
+    rs = [layer(xg) for layer in sep]
+    torch.cuda.synchronize()
+    xf = x.float().permute(0, 4, 1, 2, 3)
+    got = [out[..., :widths[0]].cpu(), h1.cpu(), h2.cpu()]
+    for gi, ri, wi, bi in zip(got, rs, ws, bs):
+        ref = F.relu(F.conv3d(xf, wi.to(T16[dt]).float(), bi)).permute(0, 2, 3, 4, 1).to(T16[dt])
+        u = _ulps(gi, ref, dt)
+        assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05, float(u.max())
+        assert _ulps(gi, ri.cpu(), dt).max() <= 1.0
+    assert out[..., widths[0]:].abs().max() == 0
+
+
 def _split_case(g, n, d, h, w, cin, widths, dt):
     from fac_fake_amd.ops import ConvLayer, conv_split
     x = torch.randn(n, d, h, w, cin, generator=g).to(T16[dt]).to(DEV)
