@@ -1141,6 +1141,120 @@ __global__ __launch_bounds__(256, 3) void maxpool2s_pw(const uint16_t* __restric
   }
 }
 
+// ---- sep_tiny (round 6): Mixed_3b's branch2 SepConv3d(16, 32, 3) on 8 x 14
+// x 14 maps (model.py:84-110: the (1,3,3) conv 16 -> 32 + BN + ReLU, then the
+// (3,1,1) conv 32 -> 32 + BN + ReLU) in one launch.  Through the generic
+// implicit GEMM these 16- / 32-channel layers ran at ~0.1 of peak with 230 MB
+// of traffic in 0.4 ms (two launches of latency-bound 16-channel gathers and
+// the 32-channel map through HBM).  Here one 512-thread workgroup per CU
+// walks clips: a clip's whole 8 x 196 x 16 input (50 KB) lands in LDS by
+// global_load_lds, the spatial conv writes its 8 x 196 x 32 map to LDS (100
+// KB), the temporal conv reads it and stores straight into the block
+// output's channel slot; the next clip's input streams in behind the
+// temporal phase.  Both convs are transposed MFMAs (rows = channels in
+// conv_pw's order, so a lane ends with 8 consecutive channels of a
+// position), with the weights in VGPRs; taps outside the frame / clip read
+// zero.  K orders as fac_conv_nd's packing: spatial k = tap * 16 + c (k_pad
+// 192: 5 steps of two taps), temporal k = dz * 32 + c.
+template <class T>
+__global__ __launch_bounds__(512, 1) void sep_tiny(const uint16_t* __restrict__ in, const uint16_t* __restrict__ ws,
+                                                   const float* __restrict__ bs, int kps, const uint16_t* __restrict__ wt,
+                                                   const float* __restrict__ bt, int kpt, uint16_t* __restrict__ out,
+                                                   int nclips, int ldo, int c_off, int relu_s, int relu_t) {
+  constexpr int S = 14, P = S * S, D = 8, NP = D * P, NT = NP / 16;  // positions per clip, 98 tiles
+  constexpr int XEL = NP * 16, MEL = NP * 32;                          // elements: input (16 ch), map (32 ch)
+  constexpr int XPL = (NP * 2 + 511) / 512;                           // glds pieces per lane per clip (6.1 -> 7)
+  __shared__ __attribute__((aligned(16))) uint16_t smem[XEL + MEL];
+  uint16_t* const xs = smem;        // [position][2 pieces]
+  uint16_t* const ms = smem + XEL;  // [position][4 pieces], piece g at g ^ ((p >> 2) & 3)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  // weights as A fragments: row r16 of channel tile ct = channel 8 (r16 >> 2) + 4 ct + (r16 & 3)
+  const int wrow = 8 * (r16 >> 2) + (r16 & 3);
+  u16x8 wsf[5][2], wtf[3][2];
+#pragma unroll
+  for (int s = 0; s < 5; ++s)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) wsf[s][ct] = *(const u16x8*)(ws + (size_t)(wrow + 4 * ct) * kps + s * 32 + g * 8);
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) wtf[s][ct] = *(const u16x8*)(wt + (size_t)(wrow + 4 * ct) * kpt + s * 32 + g * 8);
+  float bsv[2][4], btv[2][4];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bsv[ct][j] = bs ? bs[8 * g + 4 * ct + j] : 0.f;
+      btv[ct][j] = bt ? bt[8 * g + 4 * ct + j] : 0.f;
+    }
+  // a clip's input: unit q = position q >> 1, half q & 1 (16 consecutive bytes
+  // of the dense 16-channel row); units past the clip re-read its last one
+  auto issue = [&](int clip) {
+    const uint16_t* src = in + (size_t)min(clip, nclips - 1) * NP * 16;
+#pragma unroll
+    for (int i = 0; i < XPL; ++i) {
+      const int q = min((i * 8 + wave) * 64 + lane, NP * 2 - 1);
+      if ((i * 8 + wave) * 64 < NP * 2) glds16(src + q * 8, xs + (i * 8 + wave) * 64 * 8);
+    }
+  };
+  int clip = blockIdx.x;
+  if (clip < nclips) issue(clip);
+  for (; clip < nclips; clip += gridDim.x) {
+    __syncthreads();  // (vmcnt(0): this clip's input landed; the previous clip's map reads are done)
+    // spatial (1,3,3): B fragment of k-step s, lane group g = tap 2 s + (g >> 1), channel half g & 1
+    for (int t = wave; t < NT; t += 8) {
+      const int p = t * 16 + r16, z = p / P, pos = p - z * P, y = pos / S, x = pos - y * S;
+      f32x4 acc[2] = {(f32x4)0.f, (f32x4)0.f};
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        const int tap = 2 * s + (g >> 1), dy = tap / 3 - 1, dx = tap % 3 - 1;
+        const int yy = y + dy, xx = x + dx;
+        u16x8 b = (u16x8)0;
+        if (tap < 9 && (unsigned)yy < (unsigned)S && (unsigned)xx < (unsigned)S)
+          b = *(const u16x8*)(xs + ((z * P + yy * S + xx) * 2 + (g & 1)) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct] = T::mfma(wsf[s][ct], b, acc[ct]);
+      }
+      f32x4 v[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float q = acc[ct][j] + bsv[ct][j];
+          v[ct][j] = relu_s ? relu(q) : q;
+        }
+      const u16x4 lo = T::pack4(v[0]), hi = T::pack4(v[1]);
+      *(u16x8*)(ms + (p * 4 + (g ^ ((p >> 2) & 3))) * 8) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    __syncthreads();  // the map is complete; the input image is free
+    if (clip + (int)gridDim.x < nclips) issue(clip + gridDim.x);
+    // temporal (3,1,1): k-step s = frame z + s - 1, lane group g = channels 8 g .. 8 g + 7
+    for (int t = wave; t < NT; t += 8) {
+      const int p = t * 16 + r16, z = p / P;
+      f32x4 acc[2] = {(f32x4)0.f, (f32x4)0.f};
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int zz = z + s - 1, pp = p + (s - 1) * P;
+        u16x8 b = (u16x8)0;
+        if ((unsigned)zz < (unsigned)D) b = *(const u16x8*)(ms + (pp * 4 + (g ^ ((pp >> 2) & 3))) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct] = T::mfma(wtf[s][ct], b, acc[ct]);
+      }
+      f32x4 v[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float q = acc[ct][j] + btv[ct][j];
+          v[ct][j] = relu_t ? relu(q) : q;
+        }
+      const u16x4 lo = T::pack4(v[0]), hi = T::pack4(v[1]);
+      *(u16x8*)(out + ((size_t)clip * NP + p) * ldo + c_off + 8 * g) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+}
+
 // ---- input staging
 template <class T, bool U8>
 __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
@@ -3968,6 +4082,43 @@ int fac_s3d_base0_u8(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, const
     s3d_base0<F16><<<grid, 512, 0, st>>>(clip, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
                                          (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out,
                                          nunits, h, w, pad_before, rs, rt);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_sep_tiny(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, void* stream) {
+  using namespace fac;
+  if (!sdsc || !tdsc || !sdsc->in || !sdsc->weight || !tdsc->weight || !tdsc->out || sdsc->dtype != tdsc->dtype ||
+      (sdsc->dtype != FAC_DTYPE_BF16 && sdsc->dtype != FAC_DTYPE_F16))
+    return FAC_ERR_ARG;
+  if (((sdsc->flags | tdsc->flags) & ~FAC_CONV_RELU) != 0) return FAC_ERR_ARG;
+  int cps, kps, cpt, kpt;
+  fac_conv_weight_layout(sdsc->cout, sdsc->cin, sdsc->kd, sdsc->kh, sdsc->kw, &cps, &kps);
+  fac_conv_weight_layout(tdsc->cout, tdsc->cin, tdsc->kd, tdsc->kh, tdsc->kw, &cpt, &kpt);
+  const bool sp = sdsc->cin == 16 && sdsc->cout == 32 && sdsc->kd == 1 && sdsc->kh == 3 && sdsc->kw == 3 &&
+                  sdsc->sd == 1 && sdsc->sh == 1 && sdsc->sw == 1 && sdsc->pd == 0 && sdsc->ph == 1 && sdsc->pw == 1 &&
+                  sdsc->d == 8 && sdsc->h == 14 && sdsc->w == 14 && sdsc->od == 8 && sdsc->oh == 14 && sdsc->ow == 14 &&
+                  sdsc->k_pad == kps && kps == 192 && sdsc->n > 0;
+  const bool tp = tdsc->cin == 32 && tdsc->cout == 32 && tdsc->kd == 3 && tdsc->kh == 1 && tdsc->kw == 1 &&
+                  tdsc->sd == 1 && tdsc->sh == 1 && tdsc->sw == 1 && tdsc->pd == 1 && tdsc->ph == 0 && tdsc->pw == 0 &&
+                  tdsc->n == sdsc->n && tdsc->d == 8 && tdsc->h == 14 && tdsc->w == 14 && tdsc->od == 8 &&
+                  tdsc->oh == 14 && tdsc->ow == 14 && tdsc->k_pad == kpt && kpt == 128 && tdsc->ldo % 8 == 0 &&
+                  tdsc->c_off % 8 == 0 && tdsc->ldo >= tdsc->c_off + 32;
+  if (!sp || !tp) return FAC_ERR_SHAPE;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const int grid = std::min(sdsc->n, ncu);
+  const int rs = (sdsc->flags & FAC_CONV_RELU) != 0, rt = (tdsc->flags & FAC_CONV_RELU) != 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (sdsc->dtype == FAC_DTYPE_BF16)
+    sep_tiny<BF16><<<grid, 512, 0, st>>>((const uint16_t*)sdsc->in, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
+                                         (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out, sdsc->n,
+                                         tdsc->ldo, tdsc->c_off, rs, rt);
+  else
+    sep_tiny<F16><<<grid, 512, 0, st>>>((const uint16_t*)sdsc->in, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
+                                        (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out, sdsc->n,
+                                        tdsc->ldo, tdsc->c_off, rs, rt);
   return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 

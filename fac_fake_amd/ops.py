@@ -470,6 +470,42 @@ def conv_s2d4_clip(layer: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2,
     return out
 
 
+def sep_tiny_ok(spatial: ConvLayer, temporal: ConvLayer, x: torch.Tensor) -> bool:
+    """Whether fac_sep_tiny takes this SepConv3d on x: Mixed_3b's branch2
+    (1,3,3) 16 -> 32 then (3,1,1) 32 -> 32 over [N, 8, 14, 14, 16]."""
+    gs, gt = spatial.g, temporal.g
+    return (x.dim() == 5 and tuple(x.shape[1:]) == (8, 14, 14, 16) and spatial.cin_p == 16 and spatial.cout == 32
+            and (gs.kd, gs.kh, gs.kw, gs.sd, gs.sh, gs.sw, gs.pd, gs.ph, gs.pw) == (1, 3, 3, 1, 1, 1, 0, 1, 1)
+            and temporal.cin_p == 32 and temporal.cout == 32
+            and (gt.kd, gt.kh, gt.kw, gt.sd, gt.sh, gt.sw, gt.pd, gt.ph, gt.pw) == (3, 1, 1, 1, 1, 1, 1, 0, 0)
+            and _lib.exports("fac_sep_tiny"))
+
+
+def sep_tiny(spatial: ConvLayer, temporal: ConvLayer, x: torch.Tensor, out: torch.Tensor, c_off: int = 0) -> torch.Tensor:
+    """``temporal(spatial(x))`` with both ReLUs in one launch (fac_sep_tiny:
+    Mixed_3b's branch2 SepConv, the 32-channel map kept in LDS), written into
+    channels [c_off, c_off + 32) of `out` [N, 8, 14, 14, C]."""
+    if not sep_tiny_ok(spatial, temporal, x) or x.dtype != TORCH16[spatial.dtype] or not x.is_contiguous():
+        raise ValueError(f"sep_tiny needs the 16 -> 32 -> 32 SepConv over [N,8,14,14,16], got {tuple(x.shape)}")
+    if tuple(out.shape[:4]) != tuple(x.shape[:4]) or not out.is_contiguous():
+        raise ValueError("out must be contiguous [N,8,14,14,C]")
+    sd = _desc(spatial, x, None, RELU)
+    n = x.shape[0]
+    td = ConvDesc()
+    td.dtype = _lib.DTYPES[temporal.dtype]
+    td.n, td.d, td.h, td.w, td.cin = n, 8, 14, 14, temporal.cin_p
+    td.weight, td.bias = temporal.w.data_ptr(), temporal.b.data_ptr()
+    td.cout, td.k_pad = temporal.cout, temporal.k_pad
+    g = temporal.g
+    td.kd, td.kh, td.kw, td.sd, td.sh, td.sw = g.kd, g.kh, g.kw, g.sd, g.sh, g.sw
+    td.pd, td.ph, td.pw = g.pd, g.ph, g.pw
+    td.od, td.oh, td.ow = temporal.out_dims(8, 14, 14)
+    td.out, td.ldo, td.c_off = out.data_ptr(), out.shape[4], c_off
+    td.flags = RELU
+    _lib.check(_lib.load().fac_sep_tiny(ctypes.byref(sd), ctypes.byref(td), _stream(x)), None, "fac_sep_tiny")
+    return out
+
+
 def s3d_base0_u8(spatial: ConvLayer, temporal: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2,
                  pad_after: int = 1) -> torch.Tensor:
     """S3D's base.0 in one launch (fac_s3d_base0_u8): ``temporal(

@@ -135,6 +135,16 @@ int fac_conv_nd_dual(const fac_conv_desc* desc, const fac_conv_desc* ds, void* s
  * back.  FAC_ERR_ARG / FAC_ERR_SHAPE for anything else. */
 int fac_bottleneck_pw2(const fac_conv_desc* c3, const fac_conv_desc* c1, void* stream);
 
+/* S3D Mixed_3b's branch2 SepConv3d(16, 32, 3) (model.py:84-110) in one
+ * launch: sdsc = the (1,3,3) conv 16 -> 32 (+ BN folded, FAC_CONV_RELU at
+ * most) over desc->in = [n][8][14][14][16], tdsc = the (3,1,1) conv 32 -> 32
+ * over its output (tdsc->in is ignored: the 32-channel map stays in LDS),
+ * written to tdsc->out [m*ldo + c_off + c] (the block output's channel
+ * slot).  Every output is what fac_conv_nd(sdsc) then fac_conv_nd(tdsc)
+ * would produce up to fp32 summation order.  FAC_ERR_SHAPE for any other
+ * shape. */
+int fac_sep_tiny(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, void* stream);
+
 /* Weight packing geometry for fac_conv_nd: *cout_pad = cout rounded up to
  * 128, *k_pad = taps*cin rounded up to 64. */
 int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad);

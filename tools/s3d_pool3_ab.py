@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--attr", default="fuse_pool3", choices=["fuse_pool3", "fuse_pool1"],
+    ap.add_argument("--attr", default="fuse_pool3", choices=["fuse_pool3", "fuse_pool1", "fuse_sep"],
                     help="the S3D switch the arms toggle (branch3's pool, or base.1's)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
