@@ -1255,6 +1255,116 @@ __global__ __launch_bounds__(512, 1) void sep_tiny(const uint16_t* __restrict__ 
   }
 }
 
+// ---- sep_mid (round 6): Mixed_3c's branch2 SepConv3d(32, 96, 3) on 8 x 14 x
+// 14 maps (model.py:84-110), the (1,3,3) conv 32 -> 96 and the (3,1,1) conv
+// 96 -> 96, each + BN + ReLU, in one launch.  The 96-channel map of a whole
+// clip (301 KB) does not fit LDS, so a unit is (clip, 2 image rows): its 8
+// frames x 4 input rows (the band and its halo, 28 KB) land by
+// global_load_lds, the spatial conv writes the band's 8 x 28 x 96 map to LDS
+// (43 KB), and the temporal conv (which needs no spatial halo) reads it.  Six
+// waves: wave w computes output channels 32 (w % 3) .. + 31 of position tiles
+// w / 3, w / 3 + 2, ..., with its 18 + 18 weight fragments in VGPRs (the
+// layers' own packing: spatial k = tap * 32 + c, temporal k = dz * 128 + c
+// over the middle channels zero-padded to 128, of which the 96 real ones are
+// read).  Two workgroups per CU.
+template <class T>
+__global__ __launch_bounds__(384, 2) void sep_mid(const uint16_t* __restrict__ in, const uint16_t* __restrict__ ws,
+                                                  const float* __restrict__ bs, int kps, const uint16_t* __restrict__ wt,
+                                                  const float* __restrict__ bt, int kpt, uint16_t* __restrict__ out,
+                                                  int nunits, int ldo, int c_off, int relu_s, int relu_t) {
+  constexpr int S = 14, D = 8, RB = 2, NB = S / RB;  // map side, frames, rows per band, bands per clip
+  constexpr int PIN = D * (RB + 2) * S;              // input positions per unit (band + halo rows)
+  constexpr int P = D * RB * S, NT = P / 16;         // output positions per unit, 14 tiles
+  constexpr int XEL = PIN * 32, MEL = P * 96;        // elements: input (32 ch), map (96 ch)
+  constexpr int XU = PIN * 4;                         // 16-byte input units, 28 wave instructions
+  static_assert(XU % 64 == 0 && P % 16 == 0, "unit shape");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[XEL + MEL];
+  uint16_t* const xs = smem;        // [pos_in][4 pieces], piece j at j ^ ((pos_in >> 2) & 3)
+  uint16_t* const ms = smem + XEL;  // [pos][12 pieces], piece j at 4 (j >> 2) + ((j & 3) ^ ((pos >> 2) & 3))
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int cp = wave % 3, wr = wave / 3;  // channel pair (32 channels), tile row
+  const int wrow = 32 * cp + 8 * (r16 >> 2) + (r16 & 3);
+  u16x8 wsf[9][2], wtf[9][2];
+#pragma unroll
+  for (int s = 0; s < 9; ++s)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      wsf[s][ct] = *(const u16x8*)(ws + (size_t)(wrow + 4 * ct) * kps + s * 32 + g * 8);
+      wtf[s][ct] = *(const u16x8*)(wt + (size_t)(wrow + 4 * ct) * kpt + (s / 3) * 128 + (s % 3) * 32 + g * 8);
+    }
+  float bsv[2][4], btv[2][4];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bsv[ct][j] = bs ? bs[32 * cp + 8 * g + 4 * ct + j] : 0.f;
+      btv[ct][j] = bt ? bt[32 * cp + 8 * g + 4 * ct + j] : 0.f;
+    }
+  for (int u = blockIdx.x; u < nunits; u += gridDim.x) {
+    const int clip = u / NB, y0 = (u - clip * NB) * RB;
+    __syncthreads();  // the previous unit's readers are done with both images
+    for (int q0 = wave * 64; q0 < XU; q0 += 6 * 64) {
+      const int q = q0 + lane, pin = q >> 2, j = (q & 3) ^ ((pin >> 2) & 3);
+      const int z = pin / ((RB + 2) * S), rem = pin - z * (RB + 2) * S, r = rem / S, x = rem - r * S;
+      const int y = y0 - 1 + r;
+      glds16((unsigned)y < (unsigned)S ? in + ((((size_t)clip * D + z) * S + y) * S + x) * 32 + j * 8 : g_zero16,
+             xs + q0 * 8);
+    }
+    __syncthreads();  // (vmcnt(0)) the band's input landed
+    // spatial (1,3,3): k-step s = tap, lane group g = channels 8 g .. 8 g + 7
+    for (int t = wr; t < NT; t += 2) {
+      const int p = t * 16 + r16, z = p / (RB * S), rem = p - z * RB * S, ry = rem / S, x = rem - ry * S;
+      f32x4 acc[2] = {(f32x4)0.f, (f32x4)0.f};
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        const int dy = s / 3 - 1, dx = s % 3 - 1, xx = x + dx;
+        const int pin = (z * (RB + 2) + ry + 1 + dy) * S + xx;
+        u16x8 b = (u16x8)0;
+        if ((unsigned)xx < (unsigned)S) b = *(const u16x8*)(xs + (pin * 4 + (g ^ ((pin >> 2) & 3))) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct] = T::mfma(wsf[s][ct], b, acc[ct]);
+      }
+      f32x4 v[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float q = acc[ct][j] + bsv[ct][j];
+          v[ct][j] = relu_s ? relu(q) : q;
+        }
+      const u16x4 lo = T::pack4(v[0]), hi = T::pack4(v[1]);
+      *(u16x8*)(ms + (p * 12 + 4 * cp + (g ^ ((p >> 2) & 3))) * 8) = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    __syncthreads();  // the band's map is complete
+    // temporal (3,1,1): k-step s = (frame offset s / 3, channel block s % 3)
+    for (int t = wr; t < NT; t += 2) {
+      const int p = t * 16 + r16, z = p / (RB * S), rem = p - z * RB * S;
+      f32x4 acc[2] = {(f32x4)0.f, (f32x4)0.f};
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {
+        const int zz = z + s / 3 - 1, pp = p + (s / 3 - 1) * RB * S;
+        u16x8 b = (u16x8)0;
+        if ((unsigned)zz < (unsigned)D) b = *(const u16x8*)(ms + (pp * 12 + 4 * (s % 3) + (g ^ ((pp >> 2) & 3))) * 8);
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) acc[ct] = T::mfma(wtf[s][ct], b, acc[ct]);
+      }
+      f32x4 v[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float q = acc[ct][j] + btv[ct][j];
+          v[ct][j] = relu_t ? relu(q) : q;
+        }
+      const u16x4 lo = T::pack4(v[0]), hi = T::pack4(v[1]);
+      const int ry = rem / S, x = rem - ry * S;
+      *(u16x8*)(out + ((((size_t)clip * D + z) * S + y0 + ry) * S + x) * ldo + c_off + 32 * cp + 8 * g) =
+          __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+}
+
 // ---- input staging
 template <class T, bool U8>
 __global__ __launch_bounds__(256) void pack_input(const void* src, int n_img, int S, float div, float m0, float m1,
@@ -4119,6 +4229,43 @@ int fac_sep_tiny(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, void* str
     sep_tiny<F16><<<grid, 512, 0, st>>>((const uint16_t*)sdsc->in, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
                                         (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out, sdsc->n,
                                         tdsc->ldo, tdsc->c_off, rs, rt);
+  return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+}
+
+int fac_sep_mid(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, void* stream) {
+  using namespace fac;
+  if (!sdsc || !tdsc || !sdsc->in || !sdsc->weight || !tdsc->weight || !tdsc->out || sdsc->dtype != tdsc->dtype ||
+      (sdsc->dtype != FAC_DTYPE_BF16 && sdsc->dtype != FAC_DTYPE_F16))
+    return FAC_ERR_ARG;
+  if (((sdsc->flags | tdsc->flags) & ~FAC_CONV_RELU) != 0) return FAC_ERR_ARG;
+  int cps, kps, cpt, kpt;
+  fac_conv_weight_layout(sdsc->cout, sdsc->cin, sdsc->kd, sdsc->kh, sdsc->kw, &cps, &kps);
+  fac_conv_weight_layout(tdsc->cout, tdsc->cin, tdsc->kd, tdsc->kh, tdsc->kw, &cpt, &kpt);
+  const bool sp = sdsc->cin == 32 && sdsc->cout == 128 && sdsc->kd == 1 && sdsc->kh == 3 && sdsc->kw == 3 &&
+                  sdsc->sd == 1 && sdsc->sh == 1 && sdsc->sw == 1 && sdsc->pd == 0 && sdsc->ph == 1 && sdsc->pw == 1 &&
+                  sdsc->d == 8 && sdsc->h == 14 && sdsc->w == 14 && sdsc->od == 8 && sdsc->oh == 14 && sdsc->ow == 14 &&
+                  sdsc->k_pad == kps && kps == 320 && sdsc->n > 0;
+  const bool tp = tdsc->cin == 128 && tdsc->cout == 96 && tdsc->kd == 3 && tdsc->kh == 1 && tdsc->kw == 1 &&
+                  tdsc->sd == 1 && tdsc->sh == 1 && tdsc->sw == 1 && tdsc->pd == 1 && tdsc->ph == 0 && tdsc->pw == 0 &&
+                  tdsc->n == sdsc->n && tdsc->d == 8 && tdsc->h == 14 && tdsc->w == 14 && tdsc->od == 8 &&
+                  tdsc->oh == 14 && tdsc->ow == 14 && tdsc->k_pad == kpt && kpt == 384 && tdsc->ldo % 8 == 0 &&
+                  tdsc->c_off % 8 == 0 && tdsc->ldo >= tdsc->c_off + 96;
+  if (!sp || !tp) return FAC_ERR_SHAPE;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  const int nunits = sdsc->n * 7, grid = std::min(nunits, 2 * ncu);
+  const int rs = (sdsc->flags & FAC_CONV_RELU) != 0, rt = (tdsc->flags & FAC_CONV_RELU) != 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (sdsc->dtype == FAC_DTYPE_BF16)
+    sep_mid<BF16><<<grid, 384, 0, st>>>((const uint16_t*)sdsc->in, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
+                                        (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out, nunits,
+                                        tdsc->ldo, tdsc->c_off, rs, rt);
+  else
+    sep_mid<F16><<<grid, 384, 0, st>>>((const uint16_t*)sdsc->in, (const uint16_t*)sdsc->weight, sdsc->bias, kps,
+                                       (const uint16_t*)tdsc->weight, tdsc->bias, kpt, (uint16_t*)tdsc->out, nunits,
+                                       tdsc->ldo, tdsc->c_off, rs, rt);
   return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
 }
 

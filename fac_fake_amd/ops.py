@@ -470,6 +470,18 @@ def conv_s2d4_clip(layer: ConvLayer, clip: torch.Tensor, *, pad_before: int = 2,
     return out
 
 
+def sep_mid_ok(spatial: ConvLayer, temporal: ConvLayer, x: torch.Tensor) -> bool:
+    """Whether fac_sep_mid takes this SepConv3d on x: Mixed_3c's branch2
+    (1,3,3) 32 -> 96 (output rows zero-padded to 128) then (3,1,1) 128 -> 96
+    over [N, 8, 14, 14, 32]."""
+    gs, gt = spatial.g, temporal.g
+    return (x.dim() == 5 and tuple(x.shape[1:]) == (8, 14, 14, 32) and spatial.cin_p == 32 and spatial.cout == 128
+            and (gs.kd, gs.kh, gs.kw, gs.sd, gs.sh, gs.sw, gs.pd, gs.ph, gs.pw) == (1, 3, 3, 1, 1, 1, 0, 1, 1)
+            and temporal.cin_p == 128 and temporal.cout == 96
+            and (gt.kd, gt.kh, gt.kw, gt.sd, gt.sh, gt.sw, gt.pd, gt.ph, gt.pw) == (3, 1, 1, 1, 1, 1, 1, 0, 0)
+            and _lib.exports("fac_sep_mid"))
+
+
 def sep_tiny_ok(spatial: ConvLayer, temporal: ConvLayer, x: torch.Tensor) -> bool:
     """Whether fac_sep_tiny takes this SepConv3d on x: Mixed_3b's branch2
     (1,3,3) 16 -> 32 then (3,1,1) 32 -> 32 over [N, 8, 14, 14, 16]."""
@@ -482,11 +494,15 @@ def sep_tiny_ok(spatial: ConvLayer, temporal: ConvLayer, x: torch.Tensor) -> boo
 
 
 def sep_tiny(spatial: ConvLayer, temporal: ConvLayer, x: torch.Tensor, out: torch.Tensor, c_off: int = 0) -> torch.Tensor:
-    """``temporal(spatial(x))`` with both ReLUs in one launch (fac_sep_tiny:
-    Mixed_3b's branch2 SepConv, the 32-channel map kept in LDS), written into
-    channels [c_off, c_off + 32) of `out` [N, 8, 14, 14, C]."""
-    if not sep_tiny_ok(spatial, temporal, x) or x.dtype != TORCH16[spatial.dtype] or not x.is_contiguous():
-        raise ValueError(f"sep_tiny needs the 16 -> 32 -> 32 SepConv over [N,8,14,14,16], got {tuple(x.shape)}")
+    """``temporal(spatial(x))`` with both ReLUs in one launch, written into
+    channels [c_off, c_off + cout) of `out` [N, 8, 14, 14, C]: fac_sep_tiny
+    (Mixed_3b's branch2 SepConv, the 32-channel map kept in LDS) or, for
+    Mixed_3c's 32 -> 96 -> 96 one, fac_sep_mid (2-row bands, the 96-channel
+    map in LDS)."""
+    mid = sep_mid_ok(spatial, temporal, x)
+    if not (mid or sep_tiny_ok(spatial, temporal, x)) or x.dtype != TORCH16[spatial.dtype] or not x.is_contiguous():
+        raise ValueError(f"sep_tiny needs Mixed_3b's / 3c's branch2 SepConv over [N,8,14,14,16|32], got "
+                         f"{tuple(x.shape)}")
     if tuple(out.shape[:4]) != tuple(x.shape[:4]) or not out.is_contiguous():
         raise ValueError("out must be contiguous [N,8,14,14,C]")
     sd = _desc(spatial, x, None, RELU)
@@ -502,7 +518,8 @@ def sep_tiny(spatial: ConvLayer, temporal: ConvLayer, x: torch.Tensor, out: torc
     td.od, td.oh, td.ow = temporal.out_dims(8, 14, 14)
     td.out, td.ldo, td.c_off = out.data_ptr(), out.shape[4], c_off
     td.flags = RELU
-    _lib.check(_lib.load().fac_sep_tiny(ctypes.byref(sd), ctypes.byref(td), _stream(x)), None, "fac_sep_tiny")
+    fn = "fac_sep_mid" if mid else "fac_sep_tiny"
+    _lib.check(getattr(_lib.load(), fn)(ctypes.byref(sd), ctypes.byref(td), _stream(x)), None, fn)
     return out
 
 

@@ -203,8 +203,9 @@ class S3D(nn.Module):
     # base.1's pool fused into base.2's 1x1x1 conv (FAC_CONV_PREPOOL3S2) on
     # 56-wide maps; False: fac_pool_nd then the conv (A/B)
     fuse_pool1 = True
-    # Mixed_3b's branch2 SepConv (16 -> 32 -> 32 on 8 x 14 x 14) as one launch
-    # (fac_sep_tiny); False: the two fac_conv_nd launches (A/B)
+    # Mixed_3b's / 3c's branch2 SepConv (16 -> 32 -> 32 / 32 -> 96 -> 96 on
+    # 8 x 14 x 14) as one launch (fac_sep_tiny / fac_sep_mid); False: the two
+    # fac_conv_nd launches (A/B)
     fuse_sep = True
 
     def _pad64(self, c: int, level: int) -> int:
@@ -241,8 +242,8 @@ class S3D(nn.Module):
         h2 = torch.empty(n, d, h, w, hws[1], dtype=x.dtype, device=x.device)
         conv_split(blk["heads" + sfx], x, blk["head_splits" + sfx], out, 0, h1, h2)
         t1(s1(h1), out=out, c_off=o1)
-        if self.fuse_sep and ops.sep_tiny_ok(s2, t2, h2):
-            ops.sep_tiny(s2, t2, h2, out, o2)   # Mixed_3b's 16 -> 32 -> 32 SepConv in one launch
+        if self.fuse_sep and (ops.sep_tiny_ok(s2, t2, h2) or ops.sep_mid_ok(s2, t2, h2)):
+            ops.sep_tiny(s2, t2, h2, out, o2)   # Mixed_3b's / 3c's branch2 SepConv in one launch
         else:
             t2(s2(h2), out=out, c_off=o2)
         b3 = blk["b3"]

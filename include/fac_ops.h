@@ -145,6 +145,16 @@ int fac_bottleneck_pw2(const fac_conv_desc* c3, const fac_conv_desc* c1, void* s
  * shape. */
 int fac_sep_tiny(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, void* stream);
 
+/* S3D Mixed_3c's branch2 SepConv3d(32, 96, 3) (model.py:84-110) in one
+ * launch: sdsc = the (1,3,3) conv 32 -> 96 over [n][8][14][14][32] with its
+ * output channels zero-padded to 128 (cout 128: rows 96..127 zero weights
+ * and bias, which this kernel skips), tdsc = the (3,1,1) conv over those 128
+ * channels (cin 128) -> 96, written to tdsc->out [m*ldo + c_off + c]; the
+ * middle map stays in LDS.  Every output is what fac_conv_nd(sdsc) then
+ * fac_conv_nd(tdsc) would produce up to fp32 summation order.
+ * FAC_ERR_SHAPE for any other shape. */
+int fac_sep_mid(const fac_conv_desc* sdsc, const fac_conv_desc* tdsc, void* stream);
+
 /* Weight packing geometry for fac_conv_nd: *cout_pad = cout rounded up to
  * 128, *k_pad = taps*cin rounded up to 64. */
 int fac_conv_weight_layout(int cout, int cin, int kd, int kh, int kw, int* cout_pad, int* k_pad);
