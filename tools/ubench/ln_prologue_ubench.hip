@@ -9,7 +9,8 @@
 //      row sums the 5 slabs, normalises and writes the 16-bit row (58 WGs);
 //  (b) ln_prologue: the fused prologue alone -- G workgroups (the QKV GEMM's
 //      96 column tiles, or 48) each read all 58 x 5 rows and normalise them
-//      into LDS (the GEMM body that would follow is omitted);
+//      into LDS (the GEMM body that would follow is omitted; four waves, two
+//      rows per wave in flight, wave reductions);
 // each after a producer kernel that rewrites the slabs (so they are fresh
 // in L2 / MALL as after the real split-K GEMM).  Time per launch from
 // rocprofv3 --kernel-trace (the producer's own time excluded).
@@ -74,31 +75,54 @@ __global__ __launch_bounds__(256) void ln_rows(const float* __restrict__ s, cons
   }
 }
 
-// (b) every workgroup normalises all rows into LDS (the fused GEMM prologue)
+// (b) every workgroup normalises all rows into LDS (the fused GEMM prologue):
+// wave w takes rows w, w + 4, ..., two at a time, each lane 16 consecutive
+// columns (5 slabs x 4 float4 loads per row, all in flight together), mean
+// and variance by wave reductions -- no workgroup barrier until the end
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 __global__ __launch_bounds__(256) void ln_prologue(const float* __restrict__ s, const float* __restrict__ gam,
                                                    const float* __restrict__ bet, _Float16* __restrict__ sink) {
   __shared__ _Float16 a[ROWS * COLS];  // 116 KB: the GEMM's A operand
-  __shared__ float red[4];
-  for (int r = 0; r < ROWS; ++r) {
-    float v[4], sum = 0.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r0 = wave; r0 < ROWS; r0 += 8) {
+    float v[2][16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = i * 256 + threadIdx.x;
-      float t = 0.f;
+    for (int h = 0; h < 2; ++h) {
+      const int r = min(r0 + 4 * h, ROWS - 1);
 #pragma unroll
-      for (int k = 0; k < SLABS; ++k) t += s[(k * ROWS + r) * COLS + c];
-      v[i] = t;
-      sum += t;
+      for (int i = 0; i < 16; ++i) v[h][i] = 0.f;
+#pragma unroll
+      for (int k = 0; k < SLABS; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 t = *(const float4*)(s + (k * ROWS + r) * COLS + lane * 16 + 4 * i);
+          v[h][4 * i] += t.x;
+          v[h][4 * i + 1] += t.y;
+          v[h][4 * i + 2] += t.z;
+          v[h][4 * i + 3] += t.w;
+        }
     }
-    const float mean = block_sum(sum, red) * (1.f / COLS);
-    float sq = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sq += (v[i] - mean) * (v[i] - mean);
-    const float rstd = rsqrtf(block_sum(sq, red) * (1.f / COLS) + 1e-5f);
+    for (int h = 0; h < 2; ++h) {
+      const int r = r0 + 4 * h;
+      if (r >= ROWS) break;
+      float sum = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = i * 256 + threadIdx.x;
-      a[r * COLS + c] = (_Float16)((v[i] - mean) * rstd * gam[c] + bet[c]);
+      for (int i = 0; i < 16; ++i) sum += v[h][i];
+      const float mean = wsum(sum) * (1.f / COLS);
+      float sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sq += (v[h][i] - mean) * (v[h][i] - mean);
+      const float rstd = rsqrtf(wsum(sq) * (1.f / COLS) + 1e-5f);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int c = lane * 16 + i;
+        a[r * COLS + c] = (_Float16)((v[h][i] - mean) * rstd * gam[c] + bet[c]);
+      }
     }
   }
   __syncthreads();
