@@ -1045,8 +1045,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     fac::set_pool3_g(value);
     return FAC_OK;
   }
-  if (k == "pw_res") {  // 1 (default): ResNet's K = 128 / 256 conv3 + identity by pw_res; 0: convnd_pt; process-wide
-    fac::set_pw_res(value != 0);
+  if (k == "pw_res") {  // 1 (default): ResNet's K = 128 / 256 conv3 + identity by pw_res and layer2's
+                        // conv3 + strided downsample by pw_dual2; 2: pw_res only; 0: convnd_pt; process-wide
+    if (value < 0 || value > 2) return set_err(c, FAC_ERR_ARG, "pw_res must be 0, 1 or 2");
+    fac::set_pw_res((int)value);
     return FAC_OK;
   }
   if (k == "pool_lds14") {  // 1 (default): MaxPool3d(3,1,1) on 14x14 maps by maxpool3_lds14; 0: maxpool3_s1; process-wide

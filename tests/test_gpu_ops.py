@@ -360,6 +360,49 @@ def test_conv_dual_vs_torch_fp32(case, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("case", [
+    # (n, h, cout): layer2's first bottleneck end, conv3 128 -> cout at h^2 and
+    # the downsample 256 -> cout at stride 2 over the (2h)^2 block input
+    (2, 28, 512),   # the real shape (pw_dual2, four column blocks)
+    (1, 9, 256),    # 81 positions: one ragged 64-row tile
+    (5, 11, 128),   # 605 positions, one column block, ragged last tile
+])
+def test_pw_dual2_layer2(case, dt):
+    """fac_conv_nd_dual's layer2 route (ops.hip pw_dual2: both weight blocks
+    resident in LDS, the strided downsample rows gathered by global_load_lds)
+    vs PyTorch fp32 of the same operands, and vs the generic convnd_pt DUAL
+    route (fac_set_option "pw_res" 2) within one 16-bit ulp."""
+    from fac_fake_amd.ops import ConvLayer, conv_dual
+    n, hh, cout = case
+    g = torch.Generator().manual_seed(11 + cout + hh)
+    h = torch.randn(n, 128, 1, hh, hh, generator=g).to(T16[dt]).float()
+    x = torch.randn(n, 256, 1, 2 * hh, 2 * hh, generator=g).to(T16[dt]).float()
+    w3 = torch.randn(cout, 128, 1, 1, 1, generator=g) / np.sqrt(128)
+    wd = torch.randn(cout, 256, 1, 1, 1, generator=g) / np.sqrt(256)
+    b3 = torch.randn(cout, generator=g) * 0.1
+    bd = torch.randn(cout, generator=g) * 0.1
+    l3 = ConvLayer(w3, b3, 1, 0, dtype=dt, device=DEV)
+    ld = ConvLayer(wd, bd, (1, 2, 2), 0, dtype=dt, device=DEV)
+    hg = h.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    outs = {}
+    try:
+        for v in (1, 2):
+            _set_knob(b"pw_res", v, dt)
+            outs[v] = conv_dual(l3, hg, ld, xg)
+            torch.cuda.synchronize()
+            outs[v] = outs[v].cpu()
+    finally:
+        _set_knob(b"pw_res", 1, dt)
+    a = F.relu(F.conv3d(h, w3.to(T16[dt]).float(), b3))
+    r = F.conv3d(x, wd.to(T16[dt]).float(), bd, stride=(1, 2, 2))
+    ref = F.relu(a + r).permute(0, 2, 3, 4, 1).to(T16[dt])
+    u = _ulps(outs[1], ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05, float(u.max())
+    assert _ulps(outs[1], outs[2], dt).max() <= 1.0
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
 def test_conv_nd_residual_concat_and_f32(dt):
     """Bottleneck epilogue relu(relu(conv + b) + res) into a channel slot of a
     wider buffer; and fp32 output of a 1-channel conv (S3D's final layer)."""
