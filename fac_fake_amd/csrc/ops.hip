@@ -2988,17 +2988,26 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing past-the-end pieces landed before LDS is released
 }
 
+#ifndef PWD2_BN
+#define PWD2_BN 256
+#endif
+#ifndef PWD2_NB
+#define PWD2_NB 2
+#endif
 // ---- pw_dual2 (round 6): ResNet-50 layer2's first bottleneck end -- conv3
 // (1x1 128 -> 512) + bn3 + ReLU, plus the downsample (1x1 256 -> 512,
-// stride 2, over the block input at 56^2) + bn, ReLU (ResVitKan.py:146-152)
-// -- in pw_res's form: one 512-thread workgroup per CU owning a 128-column
-// block, 64-row tiles.  The downsample's weight block sits in LDS (64 KB),
-// conv3's in VGPRs (each wave's 64 columns x K 128: 64 registers), which
-// leaves room to double-buffer BOTH input streams: the conv3 rows and the
-// strided downsample rows (512 B each, every other position of the 56^2
-// map) of the next tile are issued by global_load_lds a whole tile ahead, as
-// pw_res does.  acc -> relu(acc + b3) + b_ds between the two GEMMs (the
-// reference's order, as convnd_pt DUAL).  160 KB of LDS.
+// stride 2, over the block input at 56^2) + bn, ReLU (ResVitKan.py:146-152).
+// One 512-thread workgroup per CU owns a BN-column block (4 waves across,
+// 64 columns each; 2 waves down, 16 rows each) and walks BM-row tiles.  Both
+// weight blocks live in VGPRs (each wave's 64 columns: K 128 + K 256 = 192
+// registers), the biases in LDS, so LDS holds only the input ring: the conv3
+// rows and the strided downsample rows (512 B each, every other position of
+// the 56^2 map) of the next NB - 1 tiles, issued by global_load_lds.  BN =
+// 256 makes each output row's 512 B one workgroup's contiguous stores and
+// halves the input re-reads across column blocks against 128-wide blocks
+// (measured: 128 columns x 64 rows ran at 3.1 TB/s with HBM traffic equal
+// to the algorithmic bytes).  acc -> relu(acc + b3) + b_ds between the two
+// GEMMs (the reference's order, as convnd_pt DUAL).
 template <class T>
 __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ h, const uint16_t* __restrict__ w3,
                                                    const float* __restrict__ b3, const uint16_t* __restrict__ x,
@@ -3006,18 +3015,18 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
                                                    uint16_t* __restrict__ out, int M, int kp3, int kpd, int ldo,
                                                    int c_off, int ny, int Ho, int Wo, int Hx, int Wx, int sx,
                                                    int relu1, int relu2) {
-  constexpr int K3 = 128, KD = 256, BN = 128, BM = 64, NW = 8;
+  constexpr int K3 = 128, KD = 256, BN = PWD2_BN, BM = 512 / BN * 16, NW = 8, NB = PWD2_NB;
   constexpr int KC3 = K3 / 32, KCD = KD / 32, PP3 = K3 / 8, PPD = KD / 8;  // k-steps, 16-byte pieces per row
-  constexpr int WN = BN / 64, WM = NW / WN, WPOS = BM / WM;                // 2 x 4 waves, 16 rows each
-  constexpr int WDEL = BN * KD, HEL = BM * K3, XEL = BM * KD;
-  constexpr int HPL = BM * PP3 / 512, XPL = BM * PPD / 512;  // glds pieces per lane per tile
-  constexpr int SL = 2;                                      // 16-byte stores per lane per tile
-  static_assert(WPOS == 16 && HPL * 512 == BM * PP3 && XPL * 512 == BM * PPD, "tile shape");
-  static_assert(2 * (WDEL + 2 * HEL + 2 * XEL) <= 163840, "LDS");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[WDEL + 2 * HEL + 2 * XEL];
-  uint16_t* const sd = smem;
-  uint16_t* const sh = sd + WDEL;      // [buf][BM][K3], piece p at p ^ (row & 15)
-  uint16_t* const sx_ = sh + 2 * HEL;  // [buf][BM][KD], piece p at p ^ (row & 15)
+  constexpr int WN = BN / 64, WM = NW / WN, WPOS = BM / WM;
+  constexpr int HEL = BM * K3, XEL = BM * KD;
+  constexpr int HPL = BM * PP3 / 512, XPL = BM * PPD / 512, PL = HPL + XPL;  // glds pieces per lane per tile
+  constexpr int SL = 2;                                                      // 16-byte stores per lane per tile
+  static_assert(WPOS == 16 && HPL >= 1 && HPL * 512 == BM * PP3 && XPL * 512 == BM * PPD && NB >= 2, "tile shape");
+  static_assert(8 * BN + 2 * NB * (HEL + XEL) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[4 * BN + NB * (HEL + XEL)];
+  float* const sbias = (float*)smem;         // [2][BN]: b3, b_ds
+  uint16_t* const sh = smem + 4 * BN;        // [NB][BM][K3], piece p at p ^ (row & 15)
+  uint16_t* const sx_ = sh + NB * HEL;       // [NB][BM][KD], piece p at p ^ (row & 15)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int wn = wave % WN, wm = wave / WN;
@@ -3026,55 +3035,56 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
   if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
   const int cb = b % ny, rstep = G / ny, n0 = cb * BN;
   const int nrt = (M + BM - 1) / BM;
-  // the downsample's weight block as lane-ordered fragments (wn', k-step, ct), conv_pw's channel order
-  for (int f = wave; f < WN * KCD * 4; f += NW) {
-    const int ct = f & 3, s = (f >> 2) % KCD, wq = f / (4 * KCD);
-    const int n = n0 + wq * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
-    *(u16x8*)(sd + f * 512 + lane * 8) = *(const u16x8*)(wd + (size_t)n * kpd + s * 32 + g * 8);
+  // this wave's 64 columns of both weight blocks as lane-ordered fragments
+  // (k-step, ct), conv_pw's channel order
+  u16x8 w3f[KC3][4], wdf[KCD][4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int n = n0 + wn * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
+#pragma unroll
+    for (int s = 0; s < KC3; ++s) w3f[s][ct] = *(const u16x8*)(w3 + (size_t)n * kp3 + s * 32 + g * 8);
+#pragma unroll
+    for (int s = 0; s < KCD; ++s) wdf[s][ct] = *(const u16x8*)(wd + (size_t)n * kpd + s * 32 + g * 8);
   }
-  // conv3's: this wave's 64 columns in registers
-  u16x8 w3f[KC3][4];
-#pragma unroll
-  for (int s = 0; s < KC3; ++s)
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int n = n0 + wn * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
-      w3f[s][ct] = *(const u16x8*)(w3 + (size_t)n * kp3 + s * 32 + g * 8);
-    }
-  float bv[2][8], bdv[2][8];
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = n0 + wn * 64 + 32 * hh + 8 * g + j;
-      bv[hh][j] = b3 ? b3[n] : 0.f;
-      bdv[hh][j] = bd ? bd[n] : 0.f;
-    }
+  for (int i = tid; i < 2 * BN; i += 512) {
+    const float* bp = i < BN ? b3 : bd;
+    sbias[i] = bp ? bp[n0 + (i & (BN - 1))] : 0.f;
+  }
   // the register operands have landed before the first global_load_lds (so
   // no compiler wait on them falls inside the hand-counted loop)
 #pragma unroll
-  for (int s = 0; s < KC3; ++s)
+  for (int ct = 0; ct < 4; ++ct) {
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) asm volatile("" : "+v"(w3f[s][ct]));
+    for (int s = 0; s < KC3; ++s) asm volatile("" : "+v"(w3f[s][ct]));
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(bv[hh][j]), "+v"(bdv[hh][j]));
-  int hrow[HPL], hoff[HPL], xrow[XPL], xoff[XPL];
+    for (int s = 0; s < KCD; ++s) asm volatile("" : "+v"(wdf[s][ct]));
+  }
+  int hrow[HPL], hoff[HPL];
 #pragma unroll
   for (int i = 0; i < HPL; ++i) {
     const int q = (i * NW + wave) * 64 + lane, r = q / PP3, j = q - r * PP3;
     hrow[i] = r;
     hoff[i] = (j ^ (r & 15)) * 8;
   }
-#pragma unroll
-  for (int i = 0; i < XPL; ++i) {
-    const int q = (i * NW + wave) * 64 + lane, r = q / PPD, j = q - r * PPD;
-    xrow[i] = r;
-    xoff[i] = (j ^ (r & 15)) * 8;
+  // the downsample rows go by a cursor per piece, the output position
+  // (nn, oy, ox) of the next tile to issue, advanced by rstep tiles per issue
+  // without divisions; rows past M (nn >= N) read image N - 1
+  // (piece i is XR rows below piece 0, at the same swizzled column)
+  constexpr int XR = NW * 64 / PPD;
+  static_assert(XR % 16 == 0 || XPL == 1, "pieces share the swizzle");
+  const int HW = Ho * Wo, N = M / HW, D = rstep * BM, dn = D / HW, doy = (D - dn * HW) / Wo, dox = D % Wo;
+  const int rn = XR / HW, roy = (XR - rn * HW) / Wo, rox = XR % Wo;
+  int cox, coy, cnn, xoff;
+  {
+    const int q = wave * 64 + lane, r = q / PPD, j = q - r * PPD;
+    xoff = (j ^ (r & 15)) * 8;
+    const int m = (b / ny) * BM + r;
+    cox = m % Wo;
+    coy = (m / Wo) % Ho;
+    cnn = m / HW;
   }
   // rows past M re-read row M - 1 (their stores go to the sink), tiles past
-  // the end re-read tile 0: branch-free, every lane issues HPL + XPL pieces
+  // the end re-read tile 0: branch-free, every lane issues PL pieces a tile
   auto issue = [&](int tile, int buf) {
     const int m0 = tile < nrt ? tile * BM : 0;
 #pragma unroll
@@ -3082,22 +3092,39 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
       const int m = min(m0 + hrow[i], M - 1);
       glds16(h + (size_t)m * K3 + hoff[i], sh + buf * HEL + (i * NW + wave) * 64 * 8);
     }
+    // (ox, oy, nn) + a row step (sox, soy, sn) already reduced mod (Wo, Ho)
+    auto step = [&](int& ox, int& oy, int& nn, int sox, int soy, int sn) __attribute__((always_inline)) {
+      ox += sox;
+      const int c1 = ox >= Wo;
+      ox -= c1 ? Wo : 0;
+      oy += soy + c1;
+      const int c2 = oy >= Ho;
+      oy -= c2 ? Ho : 0;
+      nn += sn + c2;
+    };
+    int ox = cox, oy = coy, nn = cnn;
 #pragma unroll
-    for (int i = 0; i < XPL; ++i) {  // output position m = (n, oy, ox) reads x at (n, sx oy, sx ox)
-      const int m = min(m0 + xrow[i], M - 1), ox = m % Wo, t1 = m / Wo, oy = t1 % Ho, nn = t1 / Ho;
-      glds16(x + (((size_t)nn * Hx + (size_t)oy * sx) * Wx + (size_t)ox * sx) * KD + xoff[i],
-             sx_ + buf * XEL + (i * NW + wave) * 64 * 8);
+    for (int i = 0; i < XPL; ++i) {  // output position (n, oy, ox) reads x at (n, sx oy, sx ox)
+      if (i) step(ox, oy, nn, rox, roy, rn);
+      const int pos = (min(nn, N - 1) * Hx + oy * sx) * Wx + ox * sx;
+      glds16(x + (size_t)pos * KD + xoff, sx_ + buf * XEL + (i * NW + wave) * 64 * 8);
     }
+    step(cox, coy, cnn, dox, doy, dn);
   };
-  __syncthreads();  // weights in
+  __syncthreads();  // biases in
   int rt = b / ny;
-  if (rt < nrt) issue(rt, 0);
-  for (int it = 0; rt < nrt; ++it, rt += rstep) {
-    const int buf = it & 1;
-    // this tile's rows landed; younger: the previous tile's SL stores
-    if (it == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(SL) : "memory");
-    issue(rt + rstep, buf ^ 1);
+  if (rt < nrt) {
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i) issue(rt + i * rstep, i);
+  }
+  for (int it = 0, buf = 0; rt < nrt; ++it, rt += rstep, buf = buf == NB - 1 ? 0 : buf + 1) {
+    // this tile's rows landed; younger: the NB - 2 tiles after it and the
+    // stores of up to NB - 1 tiles before it (counting at most two of those
+    // only waits longer)
+    if (it == 0) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * PL) : "memory");
+    else if (it == 1 || NB == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * PL + SL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * PL + 2 * SL) : "memory");
+    issue(rt + (NB - 1) * rstep, buf == 0 ? NB - 1 : buf - 1);
     f32x4 acc[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc[ct] = (f32x4)0.f;
@@ -3113,22 +3140,23 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
     }
     // conv3 done: relu(acc + b3) + b_ds, the downsample accumulates on it
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < 4; ++ct) {
+      const int nb = wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1);
+      const f32x4 b3v = *(const f32x4*)(sbias + nb), bdq = *(const f32x4*)(sbias + BN + nb);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int hh = ct >> 1, e = ct & 1;
-        float v = acc[ct][j] + bv[hh][4 * e + j];
+        float v = acc[ct][j] + b3v[j];
         if (relu1) v = relu(v);
-        acc[ct][j] = v + bdv[hh][4 * e + j];
+        acc[ct][j] = v + bdq[j];
       }
+    }
     {
       const uint16_t* a = sx_ + buf * XEL;
 #pragma unroll
       for (int s = 0; s < KCD; ++s) {
         const u16x8 pf = *(const u16x8*)(a + (r * PPD + ((s * 4 + g) ^ (r & 15))) * 8);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-          acc[ct] = T::mfma(*(const u16x8*)(sd + ((wn * KCD + s) * 4 + ct) * 512 + lane * 8), pf, acc[ct]);
+        for (int ct = 0; ct < 4; ++ct) acc[ct] = T::mfma(wdf[s][ct], pf, acc[ct]);
       }
     }
     // epilogue: relu?(acc), 16-byte stores of channels n0 + 64 wn + 32 hh + 8 g .. +7
@@ -4521,10 +4549,11 @@ int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stre
   }
   // layer2's first block (conv3 128 -> 512 at 28^2, the downsample 256 -> 512
   // at stride 2 over the 56^2 block input): pw_dual2
-  if (g_pw_res == 1 && d->cin == 128 && ds->cin == 256 && p.KD * p.KH * p.KW == 1 && q.KD * q.KH * q.KW == 1 &&
+  if (g_pw_res == 1 && d->cin == 128 && ds->cin == 256 && d->cout % PWD2_BN == 0 && p.KD * p.KH * p.KW == 1 && q.KD * q.KH * q.KW == 1 &&
       p.SD * p.SH * p.SW == 1 && q.SD == 1 && q.SH == q.SW && q.SH >= 1 && !p.PD && !p.PH && !p.PW && !q.PD &&
-      !q.PH && !q.PW && p.Kp == 128 && q.Kp == 256 && p.D == 1 && q.D == 1) {
-    const int ny2 = d->cout / 128, G2 = std::max(ny2, ncu / ny2 * ny2);
+      !q.PH && !q.PW && p.Kp == 128 && q.Kp == 256 && p.D == 1 && q.D == 1 &&
+      (long long)q.H * q.W * d->n < (1LL << 31)) {  // (x positions as int)
+    const int ny2 = d->cout / PWD2_BN, G2 = std::max(ny2, ncu / ny2 * ny2);
     const int r1 = (d->flags & FAC_CONV_RELU) != 0, r2 = (d->flags & FAC_CONV_RELU2) != 0;
     hipStream_t st2 = (hipStream_t)stream;
 #define FAC_PWD2(TT)                                                                                             \

@@ -363,9 +363,10 @@ def test_conv_dual_vs_torch_fp32(case, dt):
 @pytest.mark.parametrize("case", [
     # (n, h, cout): layer2's first bottleneck end, conv3 128 -> cout at h^2 and
     # the downsample 256 -> cout at stride 2 over the (2h)^2 block input
-    (2, 28, 512),   # the real shape (pw_dual2, four column blocks)
-    (1, 9, 256),    # 81 positions: one ragged 64-row tile
-    (5, 11, 128),   # 605 positions, one column block, ragged last tile
+    (2, 28, 512),   # the real shape (pw_dual2, two 256-column blocks)
+    (1, 9, 256),    # 81 positions: ragged last 32-row tile, one column block
+    (5, 11, 768),   # 605 positions, three column blocks, ragged last tile
+    (1, 5, 128),    # cout not a multiple of 256: stays on convnd_pt (both arms)
 ])
 def test_pw_dual2_layer2(case, dt):
     """fac_conv_nd_dual's layer2 route (ops.hip pw_dual2: both weight blocks
