@@ -32,6 +32,7 @@ void set_pool_win(int v);
 void set_pool3_zg(int v);
 void set_pool_lds14(int v);
 void set_pw_res(int v);
+void set_tk_wreg(int v);
 void set_pool3_g(int v);
 void pack_conv3x3(int dtype, int H, int ci, int co, const float* w, uint16_t* out, int bn = 0);
 void pack_stem_conv1(int dtype, const float* w, uint16_t* out);
@@ -1043,6 +1044,10 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
   if (k == "pool3_g") {  // frames per maxpool3_pw unit on 7x7 maps: 0 default (2), 1, 2 or 4; process-wide
     if (value != 0 && value != 1 && value != 2 && value != 4) return set_err(c, FAC_ERR_ARG, "pool3_g must be 0, 1, 2 or 4");
     fac::set_pool3_g(value);
+    return FAC_OK;
+  }
+  if (k == "tk_wreg") {  // 1 (default): S3D's cin-192 temporal convs with the weights in VGPRs; 0: in LDS; process-wide
+    fac::set_tk_wreg(value != 0);
     return FAC_OK;
   }
   if (k == "pw_res") {  // 1 (default): ResNet's K = 128 / 256 conv3 + identity by pw_res and layer2's

@@ -3329,7 +3329,7 @@ __device__ unsigned long long tk2_st[4][64][8][4];
   } while (0)
 #endif
 
-template <class T, int DP, int KD, int SD, int KC, int R>
+template <class T, int DP, int KD, int SD, int KC, int R, int WR = 0>
 __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ in, const uint16_t* __restrict__ w,
                                                    const float* __restrict__ bias, uint16_t* __restrict__ out,
                                                    int nunits, int S, int Cin, int kp, int ldo, int c_off, int relu_on,
@@ -3393,16 +3393,33 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
   // (row i of the wave's tile cc -- tiles 2h, 2h+1 -- computes channel
   // 32h + 8 (i >> 2) + 4 cc + (i & 3): lane group g ends with channels
   // 32h + 8g .. +7 of its position, one 16-byte store per output frame)
-  for (int c = tid; c < 64 * KS * 4; c += 512) {
-    const int n = c / (KS * 4), k8 = c - n * (KS * 4);
-    const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
-    *(u16x8*)(wts + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) =
-        *(const u16x8*)(w + (size_t)(nb * 64 + n) * kp + k8 * 8);
+  // WR (round 6; = Cin / 32 when set): the wave's own 32 channels x all KD
+  // WR k-steps live in VGPRs instead (2 KD WR fragments), so a k-step's LDS
+  // reads are the NF input frames only, not NF + 2 KD
+  const int fp = wave & 3, h = wave >> 2;
+  u16x8 wreg[WR ? KD * WR : 1][2];
+  if constexpr (WR > 0) {
+#pragma unroll
+    for (int ks = 0; ks < KD * WR; ++ks)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+        wreg[ks][cc] = *(const u16x8*)(w + (size_t)(nb * 64 + 32 * h + 8 * (r16 >> 2) + 4 * cc + (r16 & 3)) * kp +
+                                       (ks * 4 + g) * 8);
+#pragma unroll
+    for (int ks = 0; ks < KD * WR; ++ks)
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) asm volatile("" : "+v"(wreg[ks][cc]));  // landed before the first glds
+  } else {
+    for (int c = tid; c < 64 * KS * 4; c += 512) {
+      const int n = c / (KS * 4), k8 = c - n * (KS * 4);
+      const int ct = 2 * (n >> 5) + ((n >> 2) & 1), i = 4 * ((n >> 3) & 3) + (n & 3);
+      *(u16x8*)(wts + ((((k8 >> 2) * 4 + ct) * 4 + (k8 & 3)) * 16 + i) * 8) =
+          *(const u16x8*)(w + (size_t)(nb * 64 + n) * kp + k8 * 8);
+    }
   }
   if (tid < 64) bsm[tid] = bias ? bias[nb * 64 + tid] : 0.f;
   __syncthreads();
   // wave (fp, h): output frames 2fp, 2fp+1 x channels 32h .. 32h+31 (tiles 2h, 2h+1)
-  const int fp = wave & 3, h = wave >> 2;
   f32x4 bv[2];
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc) bv[cc] = *(const f32x4*)(bsm + h * 32 + 8 * g + 4 * cc);
@@ -3428,6 +3445,38 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
     issue();  // slice s + R - 1
     TK2_STAMP(2);
     const uint16_t* const sbase = ring + (s % R) * SL + rdoff;
+    if constexpr (WR > 0) {
+      static_assert(WR % KC == 0 && WR / KC <= 2, "WR: one or two steps per unit");
+      // the step's k-steps are compile-time per (step within the unit), so
+      // the register fragments are indexed statically
+      auto kbody = [&](auto csc) __attribute__((always_inline)) {
+        constexpr int CS = decltype(csc)::value;
+#pragma unroll
+        for (int kc = 0; kc < KC; ++kc) {
+          const uint16_t* cur = sbase + kc * CE;
+          u16x8 px[NF];
+#pragma unroll
+          for (int f = 0; f < NF; ++f) {
+            const int d = d0 + f;
+            px[f] = (unsigned)d < (unsigned)D ? *(const u16x8*)(cur + d * 512) : (u16x8)0;
+          }
+#pragma unroll
+          for (int t = 0; t < KD; ++t)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int f = j * SD + t;
+              if ((unsigned)(d0 + f) < (unsigned)D) {
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc)
+                  acc[j][cc] = T::mfma(wreg[t * WR + CS * KC + kc][cc], px[f], acc[j][cc]);
+              }
+            }
+        }
+      };
+      if constexpr (WR / KC == 1) kbody(std::integral_constant<int, 0>{});
+      else if (cs == 0) kbody(std::integral_constant<int, 0>{});
+      else kbody(std::integral_constant<int, 1>{});
+    } else {
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
       const int c = cs * KC + kc;
@@ -3454,6 +3503,7 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
             for (int cc = 0; cc < 2; ++cc) acc[j][cc] = T::mfma(wf[t][cc], px[f], acc[j][cc]);
           }
         }
+    }
     }
     TK2_STAMP(3);
     const bool stored = cs == SPU - 1;
@@ -3869,11 +3919,13 @@ static int g_pool_lds14 = 1;
 // process-wide (fac_set_option "pw_res"): 1 (default) the K = 128 / 256
 // bottleneck conv3 + identity by pw_res, 0 by convnd_pt (A/B)
 static int g_pw_res = 1;
+static int g_tk_wreg = 1;  // conv_tk2 with the weights in VGPRs (cin 192)
 // process-wide (fac_set_option "pool3_g"): frames per maxpool3_pw unit on
 // 7 x 7 maps, 0 = default (2), else 1 / 2 / 4 (A/B)
 static int g_pool3_g = 0;
 void set_pool3_g(int v) { g_pool3_g = v; }
 void set_pw_res(int v) { g_pw_res = v; }
+void set_tk_wreg(int v) { g_tk_wreg = v; }
 void set_pool_lds14(int v) { g_pool_lds14 = v; }
 
 template <class T>
@@ -4254,18 +4306,25 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
   conv_tk2<TT, DP, KD, SD, KC, 3><<<grid, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,  \
                                                  (uint16_t*)d->out, nunits, d->h * d->w, d->cin, k_pad, d->ldo, \
                                                  d->c_off, relu_on, nbk, nslot)
+#define FAC_TK2W(TT, DP, KD, SD, KC, WR)                                                                       \
+  conv_tk2<TT, DP, KD, SD, KC, 3, WR><<<grid, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight,  \
+                                                            d->bias, (uint16_t*)d->out, nunits, d->h * d->w,      \
+                                                            d->cin, k_pad, d->ldo, d->c_off, relu_on, nbk, nslot)
       if (d->dtype == FAC_DTYPE_BF16) {
         if (k7) FAC_TK2(BF16, 2, 7, 2, 2);
+        else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(BF16, 1, 3, 1, 3, 6);
         else if (tk2_kc == 3) FAC_TK2(BF16, 1, 3, 1, 3);
         else if (tk2_kc == 4) FAC_TK2(BF16, 1, 3, 1, 4);
         else FAC_TK2(BF16, 1, 3, 1, 2);
       } else {
         if (k7) FAC_TK2(F16, 2, 7, 2, 2);
+        else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(F16, 1, 3, 1, 3, 6);
         else if (tk2_kc == 3) FAC_TK2(F16, 1, 3, 1, 3);
         else if (tk2_kc == 4) FAC_TK2(F16, 1, 3, 1, 4);
         else FAC_TK2(F16, 1, 3, 1, 2);
       }
 #undef FAC_TK2
+#undef FAC_TK2W
       return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
     }
     if (db) {

@@ -96,6 +96,38 @@ def test_conv_nd_vs_torch_fp32(case, dt):
     assert (u > 0).float().mean() <= 0.05
 
 
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+@pytest.mark.parametrize("shape", [(2, 28, 28), (3, 7, 9), (1, 14, 14)])
+def test_conv_tk2_weights_in_vgprs_bit_identical(shape, dt):
+    """S3D's cin-192 (3,1,1) temporal conv (base.3 / Mixed_3b-3c conv_t,
+    model.py:63-82) with each wave's weight fragments in VGPRs
+    (fac_set_option "tk_wreg" 1, the default) against the same kernel reading
+    them from LDS ("tk_wreg" 0): the same MFMA order, so bit-identical, and
+    within one 16-bit ulp of PyTorch fp32.  (3, 7, 9): 63 positions, a partial
+    last 16-position unit."""
+    from fac_fake_amd.ops import ConvLayer
+    n, h, w = shape
+    g = torch.Generator().manual_seed(5 + h * w)
+    x = torch.randn(n, 192, 8, h, w, generator=g).to(T16[dt]).float()
+    wt = torch.randn(192, 192, 3, 1, 1, generator=g) / np.sqrt(576)
+    b = torch.randn(192, generator=g) * 0.1
+    layer = ConvLayer(wt, b, 1, (1, 0, 0), dtype=dt, device=DEV)
+    xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
+    outs = {}
+    try:
+        for v in (1, 0):
+            _set_knob(b"tk_wreg", v, dt)
+            outs[v] = layer(xg, relu=True)
+            torch.cuda.synchronize()
+            outs[v] = outs[v].cpu()
+    finally:
+        _set_knob(b"tk_wreg", 1, dt)
+    assert torch.equal(outs[1], outs[0])
+    ref = F.relu(F.conv3d(x, wt.to(T16[dt]).float(), b, padding=(1, 0, 0))).permute(0, 2, 3, 4, 1).to(T16[dt])
+    u = _ulps(outs[1], ref, dt)
+    assert u.max() <= 1.0 and (u > 0).float().mean() <= 0.05
+
+
 def _nd_pt_wide(value: int, dt: str):
     """fac_set_option("nd_pt_wide") is process-wide; any context sets it."""
     import ctypes
