@@ -3348,9 +3348,10 @@ __global__ __launch_bounds__(512, 1) void conv_tk2(const uint16_t* __restrict__ 
   const int nb = b_hi % nbk, slot = (b_hi / nbk) * 8 + b_lo;
   const int CH = Cin >> 5, KS = KD * CH, SPU = CH / KC;  // chunks, k-steps, steps per unit
   const int upc = (S + 15) >> 4;  // units per clip (the last one may be partial)
+  const int wts_el = WR ? 0 : KS * 2048;  // WR: no weight block in LDS, the ring takes its room
   uint16_t* const wts = smem;
-  float* const bsm = (float*)(smem + KS * 2048);
-  uint16_t* const ring = smem + KS * 2048 + 128;
+  float* const bsm = (float*)(smem + wts_el);
+  uint16_t* const ring = smem + wts_el + 128;
   const int my_units = slot < nunits ? (nunits - slot + nslot - 1) / nslot : 0;
   const int nsteps = my_units * SPU;
 
@@ -4312,13 +4313,13 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
                                                             d->cin, k_pad, d->ldo, d->c_off, relu_on, nbk, nslot)
       if (d->dtype == FAC_DTYPE_BF16) {
         if (k7) FAC_TK2(BF16, 2, 7, 2, 2);
-        else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(BF16, 1, 3, 1, 3, 6);
+        else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(BF16, 1, 3, 1, 6, 6);
         else if (tk2_kc == 3) FAC_TK2(BF16, 1, 3, 1, 3);
         else if (tk2_kc == 4) FAC_TK2(BF16, 1, 3, 1, 4);
         else FAC_TK2(BF16, 1, 3, 1, 2);
       } else {
         if (k7) FAC_TK2(F16, 2, 7, 2, 2);
-        else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(F16, 1, 3, 1, 3, 6);
+        else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(F16, 1, 3, 1, 6, 6);
         else if (tk2_kc == 3) FAC_TK2(F16, 1, 3, 1, 3);
         else if (tk2_kc == 4) FAC_TK2(F16, 1, 3, 1, 4);
         else FAC_TK2(F16, 1, 3, 1, 2);
