@@ -227,7 +227,15 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * per thread; 0 = maxpool3_s1), "pool3_zg" (output frames per thread of
  * maxpool3_s1, 0 = all, the default), "pool_win" (1 = the (1,3,3) / (3,3,3) /
  * (2,2,2) max pools by the compile-time-window kernel, the default; 0 =
- * pool_nd); every setting gives bit-identical max pools. */
+ * pool_nd); every setting gives bit-identical max pools.  Round 6:
+ * "pool_lds14" (1 = MaxPool3d(3,1,1) on 14x14 maps by maxpool3_lds14, the
+ * default; 0 = maxpool3_s1), "pool3_g" (frames per maxpool3_pw unit on 7x7
+ * maps when the pool is fused into the branch-3 1x1 conv: 0 = the default 2,
+ * 1, 2 or 4), "pw_res" (1 = ResNet-50's K 128 / 256 conv3 + identity, layer1's
+ * conv3 + downsample and S3D's merged K 192 / 256 heads on pw_res, layer2's
+ * conv3 + strided downsample on pw_dual2, the default; 2 = pw_res only; 0 =
+ * convnd_pt / conv_pw), "tk_wreg" (1 = S3D's cin-192 (3,1,1) temporal convs
+ * with the weights in VGPRs, the default; 0 = in LDS; bit-identical). */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);
