@@ -3008,20 +3008,24 @@ __global__ __launch_bounds__(512, 1) void pw_res(const uint16_t* __restrict__ in
 // (measured: 128 columns x 64 rows ran at 3.1 TB/s with HBM traffic equal
 // to the algorithmic bytes).  acc -> relu(acc + b3) + b_ds between the two
 // GEMMs (the reference's order, as convnd_pt DUAL).
-template <class T>
+// Layer3's pair (conv3 256 -> 1024 at 14^2, downsample 512 -> 1024 at
+// stride 2 over 28^2) runs the same kernel with K3 = 256, KD = 512 and 32
+// columns per wave (CW; its two weight blocks are 192 registers again): 8
+// waves across the 256 columns, 16-row tiles, one 16-byte store per lane.
+template <class T, int K3 = 128, int KD = 256, int CW = 64>
 __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ h, const uint16_t* __restrict__ w3,
                                                    const float* __restrict__ b3, const uint16_t* __restrict__ x,
                                                    const uint16_t* __restrict__ wd, const float* __restrict__ bd,
                                                    uint16_t* __restrict__ out, int M, int kp3, int kpd, int ldo,
                                                    int c_off, int ny, int Ho, int Wo, int Hx, int Wx, int sx,
                                                    int relu1, int relu2) {
-  constexpr int K3 = 128, KD = 256, BN = PWD2_BN, BM = 512 / BN * 16, NW = 8, NB = PWD2_NB;
+  constexpr int BN = PWD2_BN, NW = 8, NB = PWD2_NB, CT = CW / 16;          // CT: 16-column tiles per wave
+  constexpr int WN = BN / CW, WM = NW / WN, BM = 16 * WM, WPOS = 16;
   constexpr int KC3 = K3 / 32, KCD = KD / 32, PP3 = K3 / 8, PPD = KD / 8;  // k-steps, 16-byte pieces per row
-  constexpr int WN = BN / 64, WM = NW / WN, WPOS = BM / WM;
   constexpr int HEL = BM * K3, XEL = BM * KD;
   constexpr int HPL = BM * PP3 / 512, XPL = BM * PPD / 512, PL = HPL + XPL;  // glds pieces per lane per tile
-  constexpr int SL = 2;                                                      // 16-byte stores per lane per tile
-  static_assert(WPOS == 16 && HPL >= 1 && HPL * 512 == BM * PP3 && XPL * 512 == BM * PPD && NB >= 2, "tile shape");
+  constexpr int SL = CT / 2;                                                 // 16-byte stores per lane per tile
+  static_assert((CW == 32 || CW == 64) && WN * CW == BN && WM * WN == NW && HPL >= 1 && HPL * 512 == BM * PP3 && XPL * 512 == BM * PPD && NB >= 2, "tile shape");
   static_assert(8 * BN + 2 * NB * (HEL + XEL) <= 163840, "LDS");
   __shared__ __attribute__((aligned(16))) uint16_t smem[4 * BN + NB * (HEL + XEL)];
   float* const sbias = (float*)smem;         // [2][BN]: b3, b_ds
@@ -3035,12 +3039,12 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
   if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
   const int cb = b % ny, rstep = G / ny, n0 = cb * BN;
   const int nrt = (M + BM - 1) / BM;
-  // this wave's 64 columns of both weight blocks as lane-ordered fragments
+  // this wave's CW columns of both weight blocks as lane-ordered fragments
   // (k-step, ct), conv_pw's channel order
-  u16x8 w3f[KC3][4], wdf[KCD][4];
+  u16x8 w3f[KC3][CT], wdf[KCD][CT];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int n = n0 + wn * 64 + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = n0 + wn * CW + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
 #pragma unroll
     for (int s = 0; s < KC3; ++s) w3f[s][ct] = *(const u16x8*)(w3 + (size_t)n * kp3 + s * 32 + g * 8);
 #pragma unroll
@@ -3053,7 +3057,7 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
   // the register operands have landed before the first global_load_lds (so
   // no compiler wait on them falls inside the hand-counted loop)
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
+  for (int ct = 0; ct < CT; ++ct) {
 #pragma unroll
     for (int s = 0; s < KC3; ++s) asm volatile("" : "+v"(w3f[s][ct]));
 #pragma unroll
@@ -3071,13 +3075,14 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
   // without divisions; rows past M (nn >= N) read image N - 1
   // (piece i is XR rows below piece 0, at the same swizzled column)
   constexpr int XR = NW * 64 / PPD;
-  static_assert(XR % 16 == 0 || XPL == 1, "pieces share the swizzle");
+  static_assert(PPD % 16 == 0 && PP3 % 16 == 0, "XOR swizzles stay inside a row");
   const int HW = Ho * Wo, N = M / HW, D = rstep * BM, dn = D / HW, doy = (D - dn * HW) / Wo, dox = D % Wo;
   const int rn = XR / HW, roy = (XR - rn * HW) / Wo, rox = XR % Wo;
-  int cox, coy, cnn, xoff;
+  int cox, coy, cnn, xoff[XPL];
   {
     const int q = wave * 64 + lane, r = q / PPD, j = q - r * PPD;
-    xoff = (j ^ (r & 15)) * 8;
+#pragma unroll
+    for (int i = 0; i < XPL; ++i) xoff[i] = (j ^ ((r + i * XR) & 15)) * 8;
     const int m = (b / ny) * BM + r;
     cox = m % Wo;
     coy = (m / Wo) % Ho;
@@ -3107,7 +3112,7 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
     for (int i = 0; i < XPL; ++i) {  // output position (n, oy, ox) reads x at (n, sx oy, sx ox)
       if (i) step(ox, oy, nn, rox, roy, rn);
       const int pos = (min(nn, N - 1) * Hx + oy * sx) * Wx + ox * sx;
-      glds16(x + (size_t)pos * KD + xoff, sx_ + buf * XEL + (i * NW + wave) * 64 * 8);
+      glds16(x + (size_t)pos * KD + xoff[i], sx_ + buf * XEL + (i * NW + wave) * 64 * 8);
     }
     step(cox, coy, cnn, dox, doy, dn);
   };
@@ -3125,9 +3130,9 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
     else if (it == 1 || NB == 2) asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * PL + SL) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * PL + 2 * SL) : "memory");
     issue(rt + (NB - 1) * rstep, buf == 0 ? NB - 1 : buf - 1);
-    f32x4 acc[4];
+    f32x4 acc[CT];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) acc[ct] = (f32x4)0.f;
+    for (int ct = 0; ct < CT; ++ct) acc[ct] = (f32x4)0.f;
     const int r = wm * WPOS + r16;
     {
       const uint16_t* a = sh + buf * HEL;
@@ -3135,13 +3140,13 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
       for (int s = 0; s < KC3; ++s) {
         const u16x8 pf = *(const u16x8*)(a + (r * PP3 + ((s * 4 + g) ^ (r & 15))) * 8);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[ct] = T::mfma(w3f[s][ct], pf, acc[ct]);
+        for (int ct = 0; ct < CT; ++ct) acc[ct] = T::mfma(w3f[s][ct], pf, acc[ct]);
       }
     }
     // conv3 done: relu(acc + b3) + b_ds, the downsample accumulates on it
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const int nb = wn * 64 + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1);
+    for (int ct = 0; ct < CT; ++ct) {
+      const int nb = wn * CW + 32 * (ct >> 1) + 8 * g + 4 * (ct & 1);
       const f32x4 b3v = *(const f32x4*)(sbias + nb), bdq = *(const f32x4*)(sbias + BN + nb);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -3156,14 +3161,14 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
       for (int s = 0; s < KCD; ++s) {
         const u16x8 pf = *(const u16x8*)(a + (r * PPD + ((s * 4 + g) ^ (r & 15))) * 8);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[ct] = T::mfma(wdf[s][ct], pf, acc[ct]);
+        for (int ct = 0; ct < CT; ++ct) acc[ct] = T::mfma(wdf[s][ct], pf, acc[ct]);
       }
     }
-    // epilogue: relu?(acc), 16-byte stores of channels n0 + 64 wn + 32 hh + 8 g .. +7
+    // epilogue: relu?(acc), 16-byte stores of channels n0 + CW wn + 32 hh + 8 g .. +7
     const int m = rt * BM + r;
-    uint16_t* o = m < M ? out + (size_t)m * ldo + c_off + n0 + wn * 64 + 8 * g : g_sink + lane * 8;
+    uint16_t* o = m < M ? out + (size_t)m * ldo + c_off + n0 + wn * CW + 8 * g : g_sink + lane * 8;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
+    for (int hh = 0; hh < SL; ++hh) {
       u16x4 q[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -4609,18 +4614,23 @@ int fac_conv_nd_dual(const fac_conv_desc* d, const fac_conv_desc* ds, void* stre
   }
   // layer2's first block (conv3 128 -> 512 at 28^2, the downsample 256 -> 512
   // at stride 2 over the 56^2 block input): pw_dual2
-  if (g_pw_res == 1 && d->cin == 128 && ds->cin == 256 && d->cout % PWD2_BN == 0 && p.KD * p.KH * p.KW == 1 && q.KD * q.KH * q.KW == 1 &&
+  if (g_pw_res == 1 && ((d->cin == 128 && ds->cin == 256) || (d->cin == 256 && ds->cin == 512)) && d->cout % PWD2_BN == 0 && p.KD * p.KH * p.KW == 1 && q.KD * q.KH * q.KW == 1 &&
       p.SD * p.SH * p.SW == 1 && q.SD == 1 && q.SH == q.SW && q.SH >= 1 && !p.PD && !p.PH && !p.PW && !q.PD &&
-      !q.PH && !q.PW && p.Kp == 128 && q.Kp == 256 && p.D == 1 && q.D == 1 &&
+      !q.PH && !q.PW && p.Kp == d->cin && q.Kp == ds->cin && p.D == 1 && q.D == 1 &&
       (long long)q.H * q.W * d->n < (1LL << 31)) {  // (x positions as int)
     const int ny2 = d->cout / PWD2_BN, G2 = std::max(ny2, ncu / ny2 * ny2);
     const int r1 = (d->flags & FAC_CONV_RELU) != 0, r2 = (d->flags & FAC_CONV_RELU2) != 0;
     hipStream_t st2 = (hipStream_t)stream;
-#define FAC_PWD2(TT)                                                                                             \
-  pw_dual2<TT><<<G2, 512, 0, st2>>>(p.in, p.w, p.bias, q.in, q.w, q.bias, (uint16_t*)p.out, p.M, 128, 256, p.ldo, \
-                                     p.c_off, ny2, p.Ho, p.Wo, q.H, q.W, q.SH, r1, r2)
-    if (d->dtype == FAC_DTYPE_BF16) FAC_PWD2(BF16);
-    else FAC_PWD2(F16);
+#define FAC_PWD2(TT, K3, KD, CW)                                                                              \
+  pw_dual2<TT, K3, KD, CW><<<G2, 512, 0, st2>>>(p.in, p.w, p.bias, q.in, q.w, q.bias, (uint16_t*)p.out, p.M, K3, KD, \
+                                                 p.ldo, p.c_off, ny2, p.Ho, p.Wo, q.H, q.W, q.SH, r1, r2)
+    if (d->cin == 128) {
+      if (d->dtype == FAC_DTYPE_BF16) FAC_PWD2(BF16, 128, 256, 64);
+      else FAC_PWD2(F16, 128, 256, 64);
+    } else {
+      if (d->dtype == FAC_DTYPE_BF16) FAC_PWD2(BF16, 256, 512, 32);
+      else FAC_PWD2(F16, 256, 512, 32);
+    }
 #undef FAC_PWD2
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }

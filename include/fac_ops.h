@@ -119,9 +119,10 @@ int fac_conv_nd_split(const fac_conv_desc* desc, void* out1, int ldo1, int split
  * and ds->flags must be 0; no FAC_CONV_RESID / FAC_CONV_OUT_F32 on desc.
  * Replaces fac_conv_nd(ds) + fac_conv_nd(desc with residual = its output).
  * Layer1's 64 -> 256 pair with a stride-1 1x1 downsample runs on pw_res
- * DUAL (both weight blocks resident in LDS), layer2's 128 -> 512 conv3 with
- * the stride-2 256 -> 512 downsample (cout % 256 == 0) on pw_dual2 (both
- * weight blocks in VGPRs; fac_set_option "pw_res" 2
+ * DUAL (both weight blocks resident in LDS), layer2's 128 -> 512 and
+ * layer3's 256 -> 1024 conv3 with the stride-2 256 -> 512 / 512 -> 1024
+ * downsample (cout % 256 == 0) on pw_dual2 (both weight blocks in VGPRs;
+ * fac_set_option "pw_res" 2
  * routes it to convnd_pt for A/B, 0 routes both), the others on convnd_pt
  * DUAL. */
 int fac_conv_nd_dual(const fac_conv_desc* desc, const fac_conv_desc* ds, void* stream);

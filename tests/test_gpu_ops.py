@@ -393,25 +393,28 @@ def test_conv_dual_vs_torch_fp32(case, dt):
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
 @pytest.mark.parametrize("case", [
-    # (n, h, cout): layer2's first bottleneck end, conv3 128 -> cout at h^2 and
-    # the downsample 256 -> cout at stride 2 over the (2h)^2 block input
-    (2, 28, 512),   # the real shape (pw_dual2, two 256-column blocks)
-    (1, 9, 256),    # 81 positions: ragged last 32-row tile, one column block
-    (5, 11, 768),   # 605 positions, three column blocks, ragged last tile
-    (1, 5, 128),    # cout not a multiple of 256: stays on convnd_pt (both arms)
+    # (n, h, cout, c3, cds): a bottleneck's end, conv3 c3 -> cout at h^2 and
+    # the downsample cds -> cout at stride 2 over the (2h)^2 block input
+    (2, 28, 512, 128, 256),   # layer2's real shape (pw_dual2, two 256-column blocks)
+    (1, 9, 256, 128, 256),    # 81 positions: ragged last 32-row tile, one column block
+    (5, 11, 768, 128, 256),   # 605 positions, three column blocks, ragged last tile
+    (1, 5, 128, 128, 256),    # cout not a multiple of 256: stays on convnd_pt (both arms)
+    (2, 14, 1024, 256, 512),  # layer3's real shape (32 columns per wave, 16-row tiles)
+    (1, 9, 256, 256, 512),    # 81 positions: ragged last 16-row tile
+    (3, 5, 512, 256, 512),    # 75 positions over two column blocks
 ])
 def test_pw_dual2_layer2(case, dt):
-    """fac_conv_nd_dual's layer2 route (ops.hip pw_dual2: both weight blocks
-    resident in LDS, the strided downsample rows gathered by global_load_lds)
-    vs PyTorch fp32 of the same operands, and vs the generic convnd_pt DUAL
-    route (fac_set_option "pw_res" 2) within one 16-bit ulp."""
+    """fac_conv_nd_dual's layer2 / layer3 route (ops.hip pw_dual2: both
+    weight blocks in VGPRs, the strided downsample rows gathered by
+    global_load_lds) vs PyTorch fp32 of the same operands, and vs the generic
+    convnd_pt DUAL route (fac_set_option "pw_res" 2) within one 16-bit ulp."""
     from fac_fake_amd.ops import ConvLayer, conv_dual
-    n, hh, cout = case
+    n, hh, cout, c3, cds = case
     g = torch.Generator().manual_seed(11 + cout + hh)
-    h = torch.randn(n, 128, 1, hh, hh, generator=g).to(T16[dt]).float()
-    x = torch.randn(n, 256, 1, 2 * hh, 2 * hh, generator=g).to(T16[dt]).float()
-    w3 = torch.randn(cout, 128, 1, 1, 1, generator=g) / np.sqrt(128)
-    wd = torch.randn(cout, 256, 1, 1, 1, generator=g) / np.sqrt(256)
+    h = torch.randn(n, c3, 1, hh, hh, generator=g).to(T16[dt]).float()
+    x = torch.randn(n, cds, 1, 2 * hh, 2 * hh, generator=g).to(T16[dt]).float()
+    w3 = torch.randn(cout, c3, 1, 1, 1, generator=g) / np.sqrt(c3)
+    wd = torch.randn(cout, cds, 1, 1, 1, generator=g) / np.sqrt(cds)
     b3 = torch.randn(cout, generator=g) * 0.1
     bd = torch.randn(cout, generator=g) * 0.1
     l3 = ConvLayer(w3, b3, 1, 0, dtype=dt, device=DEV)

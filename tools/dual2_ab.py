@@ -40,19 +40,23 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--xstride", type=int, default=2, choices=[1, 2],
                     help="1: a compact 28^2 downsample input (measures the cost of the strided gather)")
+    ap.add_argument("--layer", type=int, default=2, choices=[2, 3],
+                    help="3: layer3's pair (256 -> 1024 at 14^2, downsample 512 -> 1024 over 28^2)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     dt = T16[a.dtype]
     g = torch.Generator().manual_seed(3)
-    l3 = ConvLayer(torch.randn(512, 128, 1, 1, 1, generator=g) / 11.3, torch.randn(512, generator=g) * 0.1, 1, 0,
-                   dtype=a.dtype, device=dev)
-    ld = ConvLayer(torch.randn(512, 256, 1, 1, 1, generator=g) / 16, torch.randn(512, generator=g) * 0.1,
+    c3, hw = (128, 28) if a.layer == 2 else (256, 14)
+    cds, cout = 2 * c3, 4 * c3
+    l3 = ConvLayer(torch.randn(cout, c3, 1, 1, 1, generator=g) / np.sqrt(c3), torch.randn(cout, generator=g) * 0.1,
+                   1, 0, dtype=a.dtype, device=dev)
+    ld = ConvLayer(torch.randn(cout, cds, 1, 1, 1, generator=g) / np.sqrt(cds), torch.randn(cout, generator=g) * 0.1,
                    (1, a.xstride, a.xstride), 0, dtype=a.dtype, device=dev)
-    h = torch.randn(a.n, 1, 28, 28, 128, device=dev).to(dt)
-    x = torch.randn(a.n, 1, 28 * a.xstride, 28 * a.xstride, 256, device=dev).to(dt)
-    out = torch.empty(a.n, 1, 28, 28, 512, device=dev, dtype=dt)
-    M = a.n * 28 * 28
-    nbytes = M * (128 + 256 + 512) * 2
+    h = torch.randn(a.n, 1, hw, hw, c3, device=dev).to(dt)
+    x = torch.randn(a.n, 1, hw * a.xstride, hw * a.xstride, cds, device=dev).to(dt)
+    out = torch.empty(a.n, 1, hw, hw, cout, device=dev, dtype=dt)
+    M = a.n * hw * hw
+    nbytes = M * (c3 + cds + cout) * 2
     res = {}
     try:
         for v in (1, 2):
@@ -61,7 +65,7 @@ def main():
             torch.cuda.synchronize()
             res[v] = out.clone()
         d = (res[1].float() - res[2].float()).abs().max().item()
-        print(f"layer2 dual n={a.n} {a.dtype} x stride {a.xstride}: M={M}, algorithmic {nbytes / 1e9:.3f} GB; "
+        print(f"layer{a.layer} dual n={a.n} {a.dtype} x stride {a.xstride}: M={M}, algorithmic {nbytes / 1e9:.3f} GB; "
               f"max |pw_dual2 - convnd_pt| = {d:.3e}", flush=True)
         for r in range(a.rounds):
             for v in (1, 2):
