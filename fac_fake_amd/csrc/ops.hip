@@ -3183,6 +3183,119 @@ __global__ __launch_bounds__(512, 1) void pw_dual2(const uint16_t* __restrict__ 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing past-the-end pieces landed before LDS is released
 }
 
+// ---- pw_res2 (round 6): ResNet-50 layer4's conv3 + identity, relu(relu(
+// conv1x1(h) + b3) + x) with K = 512 -> 2048 at 7^2 (ResVitKan.py:146-152),
+// pw_dual2's form with the residual in place of the downsample GEMM: 512
+// threads per CU own a 256-column block (8 waves x 32 columns, 16-row tiles),
+// each wave's 32 columns x K 512 of weights in VGPRs (128 registers: pw_res's
+// LDS-resident block would be 256 KB), biases in LDS, and the next tile's
+// input rows (1 KB each) and its 16 x 256 residual block double-buffered in
+// LDS by global_load_lds a tile ahead; one 16-byte residual read and one
+// 16-byte store per lane per tile.
+template <class T, int K = 512, int CW = 32, int BN = 256>
+__global__ __launch_bounds__(512, 1) void pw_res2(const uint16_t* __restrict__ h, const uint16_t* __restrict__ w,
+                                                  const float* __restrict__ bias, const uint16_t* __restrict__ res,
+                                                  uint16_t* __restrict__ out, int M, int kp, int ldo, int c_off,
+                                                  int ldr, int r_off, int ny, int relu1, int relu2) {
+  constexpr int NW = 8, NB = 2, CT = CW / 16, WN = BN / CW, WM = NW / WN, BM = 16 * WM;
+  constexpr int KC = K / 32, PP = K / 8, RPP = BN / 8;  // k-steps, 16-byte pieces per input / residual row
+  constexpr int HEL = BM * K, REL = BM * BN;
+  constexpr int HPL = BM * PP / 512, RPL = BM * RPP / 512, PL = HPL + RPL;  // glds pieces per lane per tile
+  constexpr int SL = CT / 2;                                                // 16-byte stores per lane per tile
+  static_assert((CW == 32 || CW == 64) && WN * CW == BN && WM * WN == NW && HPL >= 1 && RPL >= 1 &&
+                    HPL * 512 == BM * PP && RPL * 512 == BM * RPP && PP % 16 == 0 && RPP % 16 == 0,
+                "tile shape");
+  static_assert(4 * BN + 2 * NB * (HEL + REL) <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * BN + NB * (HEL + REL)];
+  float* const sbias = (float*)smem;     // [BN]
+  uint16_t* const sh = smem + 2 * BN;    // [NB][BM][K], piece p at p ^ (row & 15)
+  uint16_t* const sr = sh + NB * HEL;    // [NB][BM][BN], piece p at p ^ (row & 15)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int wn = wave % WN, wm = wave / WN;
+  const int G = gridDim.x;
+  int b = blockIdx.x;
+  if ((G & 7) == 0) b = (b & 7) * (G >> 3) + (b >> 3);
+  const int cb = b % ny, rstep = G / ny, n0 = cb * BN;
+  const int nrt = (M + BM - 1) / BM;
+  u16x8 wf[KC][CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = n0 + wn * CW + 32 * (ct >> 1) + 8 * (r16 >> 2) + 4 * (ct & 1) + (r16 & 3);
+#pragma unroll
+    for (int s = 0; s < KC; ++s) wf[s][ct] = *(const u16x8*)(w + (size_t)n * kp + s * 32 + g * 8);
+  }
+  for (int i = tid; i < BN; i += 512) sbias[i] = bias ? bias[n0 + i] : 0.f;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int s = 0; s < KC; ++s) asm volatile("" : "+v"(wf[s][ct]));  // landed before the first glds
+  // rows past M re-read row M - 1 (their stores go to the sink), tiles past
+  // the end re-read tile 0: branch-free, PL pieces per lane per tile
+  auto issue = [&](int tile, int buf) {
+    const int m0 = tile < nrt ? tile * BM : 0;
+#pragma unroll
+    for (int i = 0; i < HPL; ++i) {
+      const int q = (i * NW + wave) * 64 + lane, r = q / PP, j = q % PP;
+      const int m = min(m0 + r, M - 1);
+      glds16(h + (size_t)m * K + (j ^ (r & 15)) * 8, sh + buf * HEL + (i * NW + wave) * 64 * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      const int q = (i * NW + wave) * 64 + lane, r = q / RPP, j = q % RPP;
+      const int m = min(m0 + r, M - 1);
+      glds16(res + (size_t)m * ldr + r_off + n0 + (j ^ (r & 15)) * 8, sr + buf * REL + (i * NW + wave) * 64 * 8);
+    }
+  };
+  __syncthreads();  // biases in
+  int rt = b / ny;
+  if (rt < nrt) issue(rt, 0);
+  for (int it = 0; rt < nrt; ++it, rt += rstep) {
+    const int buf = it & 1;
+    // this tile's rows landed; younger: the previous tile's SL stores
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(SL) : "memory");
+    issue(rt + rstep, buf ^ 1);
+    f32x4 acc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[ct] = (f32x4)0.f;
+    const int r = wm * 16 + r16;
+    const uint16_t* a = sh + buf * HEL;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      const u16x8 pf = *(const u16x8*)(a + (r * PP + ((s * 4 + g) ^ (r & 15))) * 8);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[ct] = T::mfma(wf[s][ct], pf, acc[ct]);
+    }
+    // epilogue: relu2?(relu1?(acc + b) + res), 16-byte stores of channels
+    // n0 + CW wn + 32 hh + 8 g .. +7
+    const int m = rt * BM + r;
+    uint16_t* o = m < M ? out + (size_t)m * ldo + c_off + n0 + wn * CW + 8 * g : g_sink + lane * 8;
+#pragma unroll
+    for (int hh = 0; hh < SL; ++hh) {
+      const int pc = (wn * CW + 32 * hh) / 8 + g;  // residual piece of the lane's 8 channels
+      const u16x8 rv = *(const u16x8*)(sr + buf * REL + (r * RPP + (pc ^ (r & 15))) * 8);
+      const f32x4 b0 = *(const f32x4*)(sbias + wn * CW + 32 * hh + 8 * g);
+      const f32x4 b1 = *(const f32x4*)(sbias + wn * CW + 32 * hh + 8 * g + 4);
+      u16x4 q[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float t = acc[2 * hh + e][j] + (e ? b1[j] : b0[j]);
+          if (relu1) t = relu(t);
+          t += T::to_f32(rv[4 * e + j]);
+          v[j] = relu2 ? relu(t) : t;
+        }
+        q[e] = T::pack4(v);
+      }
+      *(u16x8*)(m < M ? o + 32 * hh : o) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing past-the-end pieces landed before LDS is released
+}
+
 // ---- conv_tk: S3D's temporal (kd,1,1) convs with 8 output frames (model.py:
 // 63-82, SepConv3d's conv_t + bn_t + relu_t: base.0's (7,1,1)/(2,1,1) and
 // base.3's (3,1,1) at 56^2 / 28^2 positions).  Through the generic implicit
@@ -4237,6 +4350,23 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
       else FAC_PWR(F16, 8, 128);
     }
 #undef FAC_PWR
+    return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
+  }
+  // layer4's conv3 + identity (K 512, cout % 256 == 0): pw_res2, weights in
+  // VGPRs ("pw_res" 2 routes it back to convnd_pt for A/B)
+  if (g_pw_res == 1 && !split && d->kd == 1 && d->kh == 1 && d->kw == 1 && d->sd == 1 && d->sh == 1 &&
+      d->sw == 1 && d->pd == 0 && d->ph == 0 && d->pw == 0 && (d->flags & FAC_CONV_RESID) &&
+      !(d->flags & ~(FAC_CONV_RELU | FAC_CONV_RESID | FAC_CONV_RELU2)) && k_pad == d->cin && d->cin == 512 &&
+      d->cout % 256 == 0 && d->ldo % 8 == 0 && d->c_off % 8 == 0 && d->ldr % 8 == 0 && d->r_off % 8 == 0) {
+    const int ny = d->cout / 256, ncu = cu_count(), G = std::max(ny, ncu / ny * ny);
+    const int r1 = (d->flags & FAC_CONV_RELU) != 0, r2 = (d->flags & FAC_CONV_RELU2) != 0;
+#define FAC_PWR2(TT)                                                                                            \
+  pw_res2<TT><<<G, 512, 0, st>>>((const uint16_t*)d->in, (const uint16_t*)d->weight, d->bias,                 \
+                                 (const uint16_t*)d->residual, (uint16_t*)d->out, (int)M, k_pad, d->ldo, d->c_off, \
+                                 d->ldr, d->r_off, ny, r1, r2)
+    if (d->dtype == FAC_DTYPE_BF16) FAC_PWR2(BF16);
+    else FAC_PWR2(F16);
+#undef FAC_PWR2
     return hipGetLastError() == hipSuccess ? FAC_OK : FAC_ERR_HIP;
   }
   // stride-1 1x1 convs with K = cin in {64, 128, 256}: conv_pw

@@ -79,7 +79,9 @@ extern "C" {
  * output (conv_pw: ResNet-50's K <= 256 bottleneck 1x1s), of which the
  * residual ones with cin 128 (cout % 256 == 0) or 256 (cout % 128 == 0) take
  * pw_res (ResNet-50 layer2 / layer3 conv3 + identity; fac_set_option
- * "pw_res" 0 routes them to the generic kernel for A/B). */
+ * "pw_res" 0 routes them to the generic kernel for A/B), and 1x1 residual
+ * convs with cin 512, cout % 256 == 0 (layer4's conv3 + identity) take
+ * pw_res2 (weights in VGPRs; "pw_res" 2 or 0 routes them to convnd_pt). */
 typedef struct fac_conv_desc {
   int dtype;
   const void* in;

@@ -321,11 +321,14 @@ def _set_knob(name: bytes, value: int, dt: str):
     (2, 14, 14, 256, 1024),    # layer3
     (1, 37, 41, 256, 256),     # two 128-wide column blocks, ragged
     (2, 9, 7, 128, 256),       # fewer row tiles than workgroups: most walk nothing
+    (2, 7, 7, 512, 2048),      # layer4 (pw_res2: weights in VGPRs, 16-row tiles)
+    (3, 5, 9, 512, 256),       # 135 positions: ragged last 16-row tile, one column block
+    (1, 11, 13, 512, 768),     # three column blocks, ragged
 ])
 def test_pw_res_bottleneck_conv3(n, h, w, cin, cout, dt):
     """pw_res (ResNet's conv3 + bn3 + ReLU + identity + ReLU at K = 128 /
     256: weights resident in LDS, input rows and residual blocks streamed by
-    global_load_lds) into a channel slot of a wider buffer: against PyTorch
+    global_load_lds; K = 512: pw_res2, weights in VGPRs) into a channel slot of a wider buffer: against PyTorch
     fp32 of the same 16-bit operands within one 16-bit ulp, against the
     convnd_pt route (fac_set_option pw_res = 0) within one ulp, the channels
     around the slot untouched."""
