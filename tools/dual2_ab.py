@@ -40,13 +40,13 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--xstride", type=int, default=2, choices=[1, 2],
                     help="1: a compact 28^2 downsample input (measures the cost of the strided gather)")
-    ap.add_argument("--layer", type=int, default=2, choices=[2, 3],
+    ap.add_argument("--layer", type=int, default=2, choices=[2, 3, 4],
                     help="3: layer3's pair (256 -> 1024 at 14^2, downsample 512 -> 1024 over 28^2)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     dt = T16[a.dtype]
     g = torch.Generator().manual_seed(3)
-    c3, hw = (128, 28) if a.layer == 2 else (256, 14)
+    c3, hw = {2: (128, 28), 3: (256, 14), 4: (512, 7)}[a.layer]
     cds, cout = 2 * c3, 4 * c3
     l3 = ConvLayer(torch.randn(cout, c3, 1, 1, 1, generator=g) / np.sqrt(c3), torch.randn(cout, generator=g) * 0.1,
                    1, 0, dtype=a.dtype, device=dev)
