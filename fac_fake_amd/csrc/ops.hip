@@ -4254,7 +4254,9 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     const int g7 = g_pool3_g ? g_pool3_g : 2;
     const int G = S == 14 ? 1 : (S == 7 ? (d->d % g7 == 0 ? g7 : (d->d % 2 == 0 ? 2 : 1)) : (d->d % 2 == 0 ? 2 : 1));
     const int nunits = d->n * (d->d / G);
-    const int nct = d->cout % 64 == 0 ? 2 : 1;
+    // 128 columns per workgroup where cout allows (the pooled image is built
+    // once per unit instead of once per 64-column block), else 64 / 32
+    const int nct = d->cout % 128 == 0 ? 4 : (d->cout % 64 == 0 ? 2 : 1);
     const dim3 grid((nunits + 7) / 8 * 8, d->cout / (32 * nct));
     const int relu_on = (d->flags & FAC_CONV_RELU) != 0;
     const uint16_t* in = (const uint16_t*)d->in;
@@ -4273,10 +4275,12 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
     else FAC_MPW(TT, 3, 1, NN);                \
   } while (0)
     if (d->dtype == FAC_DTYPE_BF16) {
-      if (nct == 2) FAC_MPW_S(BF16, 2);
+      if (nct == 4) FAC_MPW_S(BF16, 4);
+      else if (nct == 2) FAC_MPW_S(BF16, 2);
       else FAC_MPW_S(BF16, 1);
     } else {
-      if (nct == 2) FAC_MPW_S(F16, 2);
+      if (nct == 4) FAC_MPW_S(F16, 4);
+      else if (nct == 2) FAC_MPW_S(F16, 2);
       else FAC_MPW_S(F16, 1);
     }
 #undef FAC_MPW_S

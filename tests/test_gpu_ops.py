@@ -567,7 +567,8 @@ def test_max_pool_3x3x3_s1_lds14(dt, d, c):
     (3, 8, 14, 256, 64, 0),      # Mixed_3c
     (3, 5, 14, 64, 64, 16),      # 4b at the harness's 20 x 224^2 clips: 5 frames
     (3, 4, 7, 480, 64, 16),      # 4b at 112^2: K chunks of 64 with a half-empty last one, 4 frames per unit
-    (2, 4, 7, 528, 128, 0),      # 4f: two column blocks, a quarter-full last chunk
+    (2, 4, 7, 528, 128, 0),      # 4f: one 128-column block, a quarter-full last chunk
+    (2, 4, 7, 64, 256, 8),       # two 128-column blocks
     (2, 2, 7, 512, 64, 8),       # two frames per unit
     (2, 5, 7, 64, 96, 0),        # one frame per unit, three 32-channel blocks
     (3, 2, 3, 832, 128, 0),      # 5b / 5c at 112^2: 3 x 3 maps
