@@ -4038,7 +4038,7 @@ static int g_pool_lds14 = 1;
 // process-wide (fac_set_option "pw_res"): 1 (default) the K = 128 / 256
 // bottleneck conv3 + identity by pw_res, 0 by convnd_pt (A/B)
 static int g_pw_res = 1;
-static int g_tk_wreg = 1;  // conv_tk2 with the weights in VGPRs (cin 192)
+static int g_tk_wreg = 1;  // conv_tk2 with the weights in VGPRs (cin 128 / 192)
 // process-wide (fac_set_option "pool3_g"): frames per maxpool3_pw unit on
 // 7 x 7 maps, 0 = default (2), else 1 / 2 / 4 (A/B)
 static int g_pool3_g = 0;
@@ -4454,12 +4454,14 @@ static int conv_nd_impl(const fac_conv_desc* d, void* out1, int ldo1, int split1
         if (k7) FAC_TK2(BF16, 2, 7, 2, 2);
         else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(BF16, 1, 3, 1, 6, 6);
         else if (tk2_kc == 3) FAC_TK2(BF16, 1, 3, 1, 3);
+        else if (tk2_kc == 4 && g_tk_wreg) FAC_TK2W(BF16, 1, 3, 1, 4, 4);
         else if (tk2_kc == 4) FAC_TK2(BF16, 1, 3, 1, 4);
         else FAC_TK2(BF16, 1, 3, 1, 2);
       } else {
         if (k7) FAC_TK2(F16, 2, 7, 2, 2);
         else if (tk2_kc == 3 && g_tk_wreg) FAC_TK2W(F16, 1, 3, 1, 6, 6);
         else if (tk2_kc == 3) FAC_TK2(F16, 1, 3, 1, 3);
+        else if (tk2_kc == 4 && g_tk_wreg) FAC_TK2W(F16, 1, 3, 1, 4, 4);
         else if (tk2_kc == 4) FAC_TK2(F16, 1, 3, 1, 4);
         else FAC_TK2(F16, 1, 3, 1, 2);
       }

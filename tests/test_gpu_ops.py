@@ -97,9 +97,10 @@ def test_conv_nd_vs_torch_fp32(case, dt):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "fp16"])
-@pytest.mark.parametrize("shape", [(2, 28, 28), (3, 7, 9), (1, 14, 14)])
-def test_conv_tk2_weights_in_vgprs_bit_identical(shape, dt):
-    """S3D's cin-192 (3,1,1) temporal conv (base.3 / Mixed_3b-3c conv_t,
+@pytest.mark.parametrize("shape,cin", [((2, 28, 28), 192), ((3, 7, 9), 192), ((1, 14, 14), 192),
+                                       ((2, 14, 14), 128), ((3, 7, 9), 128)])
+def test_conv_tk2_weights_in_vgprs_bit_identical(shape, cin, dt):
+    """S3D's cin-192 / 128 (3,1,1) temporal convs (base.3 / Mixed_3b-3c conv_t,
     model.py:63-82) with each wave's weight fragments in VGPRs
     (fac_set_option "tk_wreg" 1, the default) against the same kernel reading
     them from LDS ("tk_wreg" 0): the same MFMA order, so bit-identical, and
@@ -107,10 +108,10 @@ def test_conv_tk2_weights_in_vgprs_bit_identical(shape, dt):
     last 16-position unit."""
     from fac_fake_amd.ops import ConvLayer
     n, h, w = shape
-    g = torch.Generator().manual_seed(5 + h * w)
-    x = torch.randn(n, 192, 8, h, w, generator=g).to(T16[dt]).float()
-    wt = torch.randn(192, 192, 3, 1, 1, generator=g) / np.sqrt(576)
-    b = torch.randn(192, generator=g) * 0.1
+    g = torch.Generator().manual_seed(5 + h * w + cin)
+    x = torch.randn(n, cin, 8, h, w, generator=g).to(T16[dt]).float()
+    wt = torch.randn(cin, cin, 3, 1, 1, generator=g) / np.sqrt(3 * cin)
+    b = torch.randn(cin, generator=g) * 0.1
     layer = ConvLayer(wt, b, 1, (1, 0, 0), dtype=dt, device=DEV)
     xg = x.permute(0, 2, 3, 4, 1).contiguous().to(T16[dt]).to(DEV)
     outs = {}

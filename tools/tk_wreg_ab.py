@@ -37,24 +37,26 @@ def main():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cin", type=int, default=192, choices=[128, 192])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     dt = T16[a.dtype]
     g = torch.Generator().manual_seed(3)
-    layer = ConvLayer(torch.randn(192, 192, 3, 1, 1, generator=g) / 24, torch.randn(192, generator=g) * 0.1, 1,
+    c = a.cin
+    layer = ConvLayer(torch.randn(c, c, 3, 1, 1, generator=g) / np.sqrt(3 * c), torch.randn(c, generator=g) * 0.1, 1,
                       (1, 0, 0), dtype=a.dtype, device=dev)
     try:
-        for hw in (28, 14):
-            x = torch.randn(a.n, 8, hw, hw, 192, device=dev).to(dt)
-            out = torch.empty(a.n, 8, hw, hw, 192, device=dev, dtype=dt)
-            fl = 2.0 * a.n * 8 * hw * hw * 192 * 576
+        for hw in ((28, 14) if c == 192 else (14,)):
+            x = torch.randn(a.n, 8, hw, hw, c, device=dev).to(dt)
+            out = torch.empty(a.n, 8, hw, hw, c, device=dev, dtype=dt)
+            fl = 2.0 * a.n * 8 * hw * hw * c * 3 * c
             res = {}
             for v in (1, 0):
                 knob(v, a.dtype)
                 layer(x, relu=True, out=out)
                 torch.cuda.synchronize()
                 res[v] = out.clone()
-            print(f"(3,1,1) 192->192 at {a.n} x 8 x {hw}^2 {a.dtype}: bit-identical {torch.equal(res[0], res[1])}",
+            print(f"(3,1,1) {c}->{c} at {a.n} x 8 x {hw}^2 {a.dtype}: bit-identical {torch.equal(res[0], res[1])}",
                   flush=True)
             for r in range(a.rounds):
                 for v in (1, 0):
