@@ -1046,7 +1046,7 @@ int fac_set_option(fac_ctx* c, const char* key, int value) {
     fac::set_pool3_g(value);
     return FAC_OK;
   }
-  if (k == "tk_wreg") {  // 1 (default): S3D's cin-192 temporal convs with the weights in VGPRs; 0: in LDS; process-wide
+  if (k == "tk_wreg") {  // 1 (default): S3D's cin-128 / 192 temporal convs with the weights in VGPRs; 0: in LDS; process-wide
     fac::set_tk_wreg(value != 0);
     return FAC_OK;
   }

@@ -234,8 +234,8 @@ int fac_set_stem_chunk(fac_ctx* ctx, int crops);
  * 1, 2 or 4), "pw_res" (1 = ResNet-50's K 128 / 256 conv3 + identity, layer1's
  * conv3 + downsample and S3D's merged K 192 / 256 heads on pw_res, layer2's
  * conv3 + strided downsample on pw_dual2, the default; 2 = pw_res only; 0 =
- * convnd_pt / conv_pw), "tk_wreg" (1 = S3D's cin-192 (3,1,1) temporal convs
- * with the weights in VGPRs, the default; 0 = in LDS; bit-identical). */
+ * convnd_pt / conv_pw), "tk_wreg" (1 = S3D's cin-128 / 192 (3,1,1) temporal
+ * convs with the weights in VGPRs, the default; 0 = in LDS; bit-identical). */
 int fac_set_option(fac_ctx* ctx, const char* key, int value);
 
 const char* fac_last_error(fac_ctx* ctx);
